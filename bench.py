@@ -1,0 +1,250 @@
+"""RAFT 12-iteration inference throughput on MI355X (BASELINE.json metric), one process per GPU.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload sintel|kitti|corr]
+    torchrun --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 --master-port P bench.py --gpus N ...
+
+Default workload "sintel" = BASELINE configs[3] per rank: every GPU infers 8 Sintel pairs (436x1024, padded
+440x1024 in predict.py's 'sintel' mode) per step, 12 GRU iterations, fp32, test_mode; the global batch is 8*N
+pairs (weak scaling; N = 8 is configs[3]'s 64 pairs). A step is: rank 0 scatters the pairs over RCCL (inputs
+resident in rank 0's HBM), every rank pads -> RAFT forward -> unpads, flows are gathered back to rank 0. With
+N = 1 there is no collective. Synthetic frames (integer texture, known shift) and hash-generated weights: no
+dataset or checkpoint is reachable offline.
+
+Printed (rank 0, one JSON line): pairs/s for the whole job, the lookup kernel's roofline (algorithmic bytes per
+launch / mean launch time from HIP events recorded on the launch stream inside the timed region), the corr
+pyramid kernel's MFMA rate, and the oracle (PyTorch-CPU restatement) timed on this host's cores.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import statistics
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+PKG = os.path.join(REPO, "torch-optical-flow_amd")
+for _p in (REPO, PKG, os.path.join(PKG, "methods", "raft")):
+    if _p not in sys.path:
+        sys.path.insert(0, _p)
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+METRIC = "image-pairs/sec + corr-lookup HBM GB/s, RAFT 12-iter @ Sintel 1024×436"
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+MFMA_F32_PEAK_TFLOPS = 157.3  # dense fp32 MFMA (v_mfma_f32_32x32x2_f32), spec
+PMC_TRAFFIC_FILE = os.path.join(REPO, "profiles", "lookup_traffic.json")
+
+WORKLOADS = {
+    # name: (pairs per GPU, H, W, iters, padder mode)
+    "sintel": (8, 436, 1024, 12, "sintel"),
+    "kitti": (8, 375, 1242, 12, "sintel"),
+}
+
+
+def lookup_bytes(batch: int, dims, radius: int = 4, s_corr: int = 4) -> int:
+    """B*N*[sum_l min(2r+2,H_l)*min(2r+2,W_l)*s_corr + 8 + L*(2r+1)^2*4] per launch."""
+    h0, w0 = dims[0]
+    n = h0 * w0
+    p = 2 * radius + 2
+    k = 2 * radius + 1
+    per_q = sum(min(p, h) * min(p, w) * s_corr for h, w in dims) + 8 + len(dims) * k * k * 4
+    return batch * n * per_q
+
+
+def pyramid_cost(batch: int, dims, c: int = 256):
+    h0, w0 = dims[0]
+    n = h0 * w0
+    flops = 2 * batch * n * n * c
+    write = batch * n * sum(h * w for h, w in dims) * 4
+    read = 2 * batch * n * c * 4
+    return flops, write + read
+
+
+def mean_ms(events) -> float:
+    return statistics.fmean(a.elapsed_time(b) for a, b in events)
+
+
+def cpu_baseline(h: int, w: int, iters: int):
+    """The oracle RAFT (PyTorch-CPU fp32, this host's threads) on 1 pair: 1 warm-up + median of 3 (~10-20 s)."""
+    from model import synthetic
+    from oracle import raft as oraft
+
+    threads = torch.get_num_threads()
+    model = oraft.RAFT().eval()
+    model.load_state_dict(synthetic.synthetic_state_dict(model.state_dict()))
+    img0, img1 = synthetic.synthetic_pair(1, h, w)
+    padder = oraft.InputPadder(img0.shape)
+    p0, p1 = padder.pad(img0, img1)
+    times = []
+    with torch.inference_mode():
+        for i in range(4):
+            t = time.perf_counter()
+            model(p0, p1, iters=iters, test_mode=True)
+            if i:
+                times.append(time.perf_counter() - t)
+    sec = statistics.median(times)
+    return {
+        "value": round(1.0 / sec, 4),
+        "unit": "image-pairs/s",
+        "cores": threads,
+        "kind": "port",
+        "sample": f"oracle RAFT (PyTorch-CPU fp32 restatement of the reference), 1 pair {h}x{w} padded, "
+        f"{iters} iters, test_mode; median of 3 after 1 warm-up ({sec:.2f} s/pair); torch threads={threads}",
+    }
+
+
+def main() -> int:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--workload", default="sintel", choices=sorted(WORKLOADS))
+    ap.add_argument("--pairs-per-gpu", type=int, default=None)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-events", action="store_true", help="do not record per-kernel HIP events")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        print(f"bench: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
+        return 2
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    from model import RAFT, InputPadder, synthetic
+    from model.pair_sharding import infer_sharded
+    from optical_flow import _native
+
+    ppg, h, w, iters, pmode = WORKLOADS[args.workload]
+    ppg = args.pairs_per_gpu or ppg
+    global_batch = ppg * world
+
+    model = RAFT().eval()
+    model.load_state_dict(synthetic.synthetic_state_dict(model.state_dict()))
+    model = model.to(dev)
+
+    img0 = img1 = None
+    if rank == 0:  # two distinct pairs tiled to the global batch, resident in rank 0's HBM
+        a0, a1 = synthetic.synthetic_pair(2, h, w, seed=0)
+        reps = -(-global_batch // 2)
+        img0 = a0.to(dev).repeat(reps, 1, 1, 1)[:global_batch].contiguous()
+        img1 = a1.to(dev).repeat(reps, 1, 1, 1)[:global_batch].contiguous()
+    padder = InputPadder((h, w), mode=pmode)
+
+    def forward(s0, s1):
+        p0, p1 = padder.pad(s0, s1)
+        low, up = model(p0, p1, iters=iters, test_mode=True)
+        return low, padder.unpad(up)
+
+    def step():
+        if world > 1:
+            return infer_sharded(forward, img0, img1, dev)
+        return forward(img0, img1)
+
+    with torch.inference_mode():
+        for _ in range(args.warmup):
+            step()
+        torch.cuda.synchronize(dev)
+        rec = {} if not args.no_events else None
+        _native.set_event_recorder(rec)
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            out = step()
+        torch.cuda.synchronize(dev)
+        if world > 1:
+            dist.barrier()
+        elapsed = time.perf_counter() - t0
+        _native.set_event_recorder(None)
+
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    if rank == 0:
+        assert out[1] is not None and out[1].shape == (global_batch, 2, h, w)
+        assert torch.isfinite(out[1]).all()
+    dims = _native.pyramid_dims((h + 7) // 8, (w + 7) // 8, 4)
+    pairs = global_batch * args.steps
+    line = {
+        "metric": METRIC,
+        "value": round(pairs / elapsed, 3),
+        "unit": "image-pairs/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(1000.0 * elapsed / args.steps, 3),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "synthetic (integer texture frames with a known (3, -1.5) px shift; hash-initialised weights)",
+        "config": {
+            "workload": f"raft-{iters}iter-{args.workload}-{h}x{w}",
+            "pairs_per_gpu": ppg,
+            "global_batch": global_batch,
+            "iters": iters,
+            "padded": f"{dims[0][0] * 8}x{dims[0][1] * 8}",
+            "parallelism": f"pairs sharded over {world} GPU(s)" + (", RCCL scatter/gather" if world > 1 else ""),
+        },
+    }
+    if rec:
+        lk = rec.get("corr_lookup", [])
+        pk = rec.get("corr_pyramid", [])
+        lk_ms = mean_ms(lk)
+        lk_bytes = lookup_bytes(ppg, dims)
+        ach = lk_bytes / (lk_ms * 1e-3) / 1e9
+        traffic = None
+        if os.path.exists(PMC_TRAFFIC_FILE):
+            with open(PMC_TRAFFIC_FILE) as f:
+                tr = json.load(f).get(f"{args.workload}:{ppg}")
+            traffic = tr.get("hbm_bytes_per_launch") if tr else None
+        line["roofline"] = {
+            "kernel": "corr_lookup",
+            "bound": "hbm",
+            "achieved": round(ach, 1),
+            "peak": HBM_PEAK_GBS,
+            "unit": "GB/s",
+            "frac": round(ach / HBM_PEAK_GBS, 4),
+            "traffic": traffic,
+            "algorithmic_bytes_per_launch": lk_bytes,
+            "launch_ms": round(lk_ms, 5),
+            "launches": len(lk),
+        }
+        if pk:
+            pk_ms = mean_ms(pk)
+            flops, nbytes = pyramid_cost(ppg, dims)
+            tf = flops / (pk_ms * 1e-3) / 1e12
+            line["kernels"] = {
+                "corr_pyramid": {
+                    "bound": "mfma",
+                    "launch_ms": round(pk_ms, 4),
+                    "achieved_tflops": round(tf, 2),
+                    "peak_tflops": MFMA_F32_PEAK_TFLOPS,
+                    "frac": round(tf / MFMA_F32_PEAK_TFLOPS, 4),
+                    "hbm_gbs": round(nbytes / (pk_ms * 1e-3) / 1e9, 1),
+                    "flops_per_launch": flops,
+                    "bytes_per_launch": nbytes,
+                }
+            }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        line["cpu_baseline"] = cpu_baseline(h, w, iters)
+    if rank == 0:
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -1,0 +1,100 @@
+/*
+ * oflow.h — C ABI of liboflow_hip.so, the MI355X (gfx950) implementation of the RAFT inference hot path of
+ * awaelchli/torch-optical-flow. Plain pointers and sizes only: no torch or C++ types cross this boundary.
+ *
+ * All pointers named d_* are DEVICE pointers (HBM), contiguous, fp32 unless stated. Every entry point only
+ * ENQUEUES work on `stream` (hipStream_t passed as void*; NULL = the null stream of the current device) and
+ * returns without synchronising; it never allocates. Callers set the current device to the one owning the
+ * buffers (the Python host layer does this with a torch device guard).
+ *
+ * Return value: OFLOW_OK (0), a negative OFLOW_E_* argument error (nothing was enqueued), or a positive
+ * hipError_t from the launch. oflow_status_string() turns either into text; the Python layer raises
+ * RuntimeError/ValueError with it, the exception types the reference's ATen ops raise.
+ *
+ * Replaces (reference file:line, /root/reference):
+ *   oflow_corr_pyramid_f32  <- methods/raft/model/corr.py:38-54 (CorrBlock.__init__) + 79-87 (CorrBlock.corr)
+ *   oflow_corr_lookup_f32   <- methods/raft/model/corr.py:56-77 (CorrBlock.__call__)
+ *                              + methods/raft/model/utils.py:64-80 (bilinear_sampler)
+ *   oflow_grid_warp_f32     <- optical_flow/operator/operator.py:8-56 (warp, warp_grid -> F.grid_sample)
+ */
+#ifndef OFLOW_H_
+#define OFLOW_H_
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define OFLOW_ABI_VERSION 1
+
+#define OFLOW_OK 0
+#define OFLOW_E_NULL (-1)      /* a required pointer is NULL */
+#define OFLOW_E_SHAPE (-2)     /* a size is <= 0 or inconsistent */
+#define OFLOW_E_LEVELS (-3)    /* num_levels outside [1, OFLOW_MAX_LEVELS] */
+#define OFLOW_E_TINY (-4)      /* a pyramid level is < 2 pixels in H or W (reference divides by 0: Q3) */
+#define OFLOW_E_RADIUS (-5)    /* radius outside [0, OFLOW_MAX_RADIUS] */
+#define OFLOW_E_MODE (-6)      /* unknown interpolation or padding mode */
+#define OFLOW_E_ALIGN (-7)     /* a pointer is not 4-byte aligned */
+
+#define OFLOW_MAX_LEVELS 8
+#define OFLOW_MAX_RADIUS 7
+
+/* grid_sample modes (torch.nn.functional.grid_sample names) */
+#define OFLOW_INTERP_BILINEAR 0
+#define OFLOW_INTERP_NEAREST 1
+#define OFLOW_INTERP_BICUBIC 2
+#define OFLOW_PAD_ZEROS 0
+#define OFLOW_PAD_BORDER 1
+#define OFLOW_PAD_REFLECTION 2
+
+int oflow_abi_version(void);
+const char* oflow_status_string(int status);
+
+/*
+ * Pyramid level sizes for a (H, W) query grid: level 0 = (H, W), level l = floor-halves of level l-1
+ * (avg_pool2d(2, stride=2) semantics, corr.py:53). Writes num_levels entries to level_h / level_w (host).
+ */
+int oflow_corr_pyramid_dims(int H, int W, int num_levels, int* level_h, int* level_w);
+
+/*
+ * All-pairs correlation pyramid (CorrBlock.__init__).
+ *   d_fmap1, d_fmap2 : (B, C, H, W) fp32
+ *   d_levels[l]      : host array of num_levels device pointers; level l is (B*H*W, H_l, W_l) fp32,
+ *                      i.e. the reference's corr_pyramid[l] of shape (B*H*W, 1, H_l, W_l).
+ *   level 0 = (fmap1^T fmap2) / sqrt(C) on fp32 MFMA (v_mfma_f32_32x32x2f32); levels 1.. are the floor
+ *   2x2 average pools of the level above, fused in the GEMM epilogue (level 0 is never re-read).
+ */
+int oflow_corr_pyramid_f32(const float* d_fmap1, const float* d_fmap2, int B, int C, int H, int W,
+                           int num_levels, float* const* d_levels, void* stream);
+
+/*
+ * Windowed multi-level bilinear lookup (CorrBlock.__call__).
+ *   d_levels[l] : as produced above (H_l, W_l from oflow_corr_pyramid_dims)
+ *   d_coords    : (B, 2, H, W) fp32 pixel coordinates, channel 0 = x, 1 = y
+ *   d_out       : (B, num_levels*(2r+1)^2, H, W) fp32; channel l*(2r+1)^2 + i*(2r+1) + j samples level l
+ *                 at (x/2^l + i - r, y/2^l + j - r), bilinear, zero outside the level (grid_sample
+ *                 align_corners=True, padding_mode='zeros').
+ */
+int oflow_corr_lookup_f32(const float* const* d_levels, const int* level_h, const int* level_w,
+                          int num_levels, const float* d_coords, int B, int H, int W, int radius,
+                          float* d_out, void* stream);
+
+/*
+ * Inverse warp (optical_flow.warp): out = grid_sample(frame, linspace-grid + flow, mode, padding_mode,
+ * align_corners). d_frame, d_out: (B, C, H, W); d_flow: (B, 2, H, W) already normalized to [-1, 1] units.
+ */
+int oflow_grid_warp_f32(const float* d_frame, const float* d_flow, int B, int C, int H, int W, int mode,
+                        int padding_mode, int align_corners, float* d_out, void* stream);
+
+/*
+ * Explicit-grid sampling (F.grid_sample): d_input (B, C, H, W), d_grid (B, Ho, Wo, 2) in [-1, 1] units
+ * (x, y), d_out (B, C, Ho, Wo). Replaces the grid_sample inside methods/raft/model/utils.py:64-80
+ * (bilinear_sampler, called there with align_corners=True, zeros padding) for callers outside CorrBlock.
+ */
+int oflow_grid_sample_f32(const float* d_input, const float* d_grid, int B, int C, int H, int W, int Ho, int Wo,
+                          int mode, int padding_mode, int align_corners, float* d_out, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* OFLOW_H_ */

@@ -1,0 +1,256 @@
+"""Parity of the gfx950 HIP path (through the C ABI of liboflow_hip.so) against the oracle and the goldens the
+reference produced. Tolerances: corr pyramid fp32 |d| <= 1e-4 + 1e-5|ref|; lookup |d| <= 1e-4;
+warp (0..255 frames) |d| <= 2e-3 (the reference's own CPU linspace is vector-width dependent at the ulp level);
+end-to-end mean EPE <= 1e-4 px... see the individual tests.
+"""
+import math
+
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+import optical_flow
+from model import CorrBlock, bilinear_sampler, synthetic
+from model.utils import coords_grid
+from optical_flow import _native
+from oracle import corr as ocorr
+from oracle import operator as oop
+
+pytestmark = pytest.mark.gpu
+DEV = torch.device("cuda", 0)
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _need_gpu():
+    assert torch.cuda.is_available(), "GPU tests need a ROCm GPU"
+    _native.load()
+
+
+def _assert_pyr(got, ref, what):
+    ref = np.asarray(ref)
+    got = got.detach().cpu().numpy()
+    assert got.shape == ref.shape, (what, got.shape, ref.shape)
+    err = np.abs(got - ref)
+    tol = 1e-4 + 1e-5 * np.abs(ref)
+    assert np.all(err <= tol), f"{what}: max err {err.max()} (worst excess {(err - tol).max()})"
+
+
+# ----------------------------------------------------------------------------------------------------------
+# correlation pyramid
+# ----------------------------------------------------------------------------------------------------------
+@pytest.mark.parametrize("tag", ["a", "b"])
+def test_pyramid_matches_reference_goldens(golden, tag):
+    g = golden("corr_small")
+    b, c, h, w = (int(v) for v in g[f"{tag}_shape"])
+    f1, f2 = synthetic.synthetic_fmaps(b, c, h, w, stream=int(g[f"{tag}_stream"]))
+    cb = CorrBlock(f1.to(DEV), f2.to(DEV), num_levels=4, radius=4)
+    for lvl in range(4):
+        _assert_pyr(cb.corr_pyramid[lvl], g[f"{tag}_pyr{lvl}"], f"{tag} level {lvl}")
+
+
+@pytest.mark.parametrize(
+    "shape,levels",
+    [
+        ((1, 256, 23, 37), 4),  # W % 4 != 0: scalar staging path, ragged tiles
+        ((2, 64, 16, 20), 4),  # C = 64
+        ((1, 100, 17, 19), 3),  # sqrt(C) = 10, not a power of two: true division
+        ((1, 256, 33, 70), 6),  # levels >= 4 through the stand-alone pooling kernel
+        ((3, 256, 9, 12), 1),
+        ((1, 7, 31, 64), 2),  # C not a multiple of the 16-channel stage
+    ],
+)
+def test_pyramid_matches_oracle_shapes(shape, levels):
+    b, c, h, w = shape
+    f1, f2 = synthetic.synthetic_fmaps(b, c, h, w, stream=31 + c)
+    ref = ocorr.corr_pyramid(f1, f2, levels)
+    got = _native.corr_pyramid(f1.to(DEV), f2.to(DEV), levels)
+    for lvl in range(levels):
+        _assert_pyr(got[lvl], ref[lvl].numpy(), f"{shape} level {lvl}")
+
+
+def test_corr_staticmethod_and_views():
+    f1, f2 = synthetic.synthetic_fmaps(2, 256, 16, 24, stream=3)
+    vol = CorrBlock.corr(f1.to(DEV), f2.to(DEV))
+    assert vol.shape == (2, 16, 24, 1, 16, 24)
+    _assert_pyr(vol, ocorr.corr_volume(f1, f2).numpy(), "corr volume")
+
+
+def test_pyramid_exact_properties():
+    """Bit-exact, size-independent properties at a Sintel-size shape (55 x 128, batch 2):
+    symmetry corr(f1,f2)[i,j] == corr(f2,f1)[j,i] (same k-ordered fp32 fma chain), linearity under a power of
+    two, and every pooled level == avg_pool2d(level above) computed by ATen on the GPU."""
+    f1, f2 = synthetic.synthetic_fmaps(2, 256, 55, 128, stream=41)
+    f1, f2 = f1.to(DEV), f2.to(DEV)
+    p = _native.corr_pyramid(f1, f2, 4)
+    pt = _native.corr_pyramid(f2, f1, 1)[0]
+    n = 55 * 128
+    a = p[0].view(2, n, n)
+    assert torch.equal(a, pt.view(2, n, n).transpose(1, 2))
+    p2 = _native.corr_pyramid(2 * f1, f2, 1)[0]
+    assert torch.equal(p2, 2 * p[0])
+    for lvl in range(1, 4):
+        assert torch.equal(p[lvl], F.avg_pool2d(p[lvl - 1], 2, stride=2)), lvl
+
+
+# ----------------------------------------------------------------------------------------------------------
+# lookup
+# ----------------------------------------------------------------------------------------------------------
+def test_lookup_matches_reference_goldens(golden):
+    g = golden("corr_small")
+    for tag in ("a", "b"):
+        pyr = [torch.from_numpy(g[f"{tag}_pyr{lvl}"]).to(DEV) for lvl in range(4)]
+        for k in [k for k in g if k.startswith(f"{tag}_coords_") and k != "a_coords_r2"]:
+            out = _native.corr_lookup(pyr, torch.from_numpy(g[k]).to(DEV), 4).cpu().numpy()
+            ref = g[k.replace("coords", "lookup")]
+            err = np.abs(out - ref).max()
+            assert err <= 1e-4, (k, err)
+    pyr3 = [torch.from_numpy(g[f"a_pyr{lvl}"]).to(DEV) for lvl in range(3)]
+    out = _native.corr_lookup(pyr3, torch.from_numpy(g["a_coords_r2"]).to(DEV), 2).cpu().numpy()
+    assert np.abs(out - g["a_lookup_r2_l3"]).max() <= 1e-4
+
+
+@pytest.mark.parametrize("radius", [0, 1, 3, 4, 7])
+@pytest.mark.parametrize("sigma", [0.0, 2.5, 30.0])
+def test_lookup_matches_oracle(radius, sigma):
+    b, h, w = 2, 19, 26
+    f1, f2 = synthetic.synthetic_fmaps(b, 64, h, w, stream=5)
+    pyr = ocorr.corr_pyramid(f1, f2, 4)
+    coords = ocorr.coords_grid(b, h, w) + torch.from_numpy(synthetic.hash_normal(70 + radius, (b, 2, h, w), sigma))
+    ref = ocorr.corr_lookup(pyr, coords, radius)
+    got = _native.corr_lookup([p.to(DEV) for p in pyr], coords.to(DEV), radius)
+    assert got.shape == ref.shape
+    assert (got.cpu() - ref).abs().max().item() <= 1e-4
+
+
+def test_lookup_window_channel_order_q1():
+    vol = torch.zeros(1, 1, 16, 16)
+    vol[0, 0, 8 + 3, 8 + 1] = 1.0
+    out = _native.corr_lookup([vol.to(DEV)], torch.tensor([8.0, 8.0]).view(1, 2, 1, 1).to(DEV), 4)
+    assert int(out.view(-1).argmax()) == 5 * 9 + 7 and float(out.sum()) == 1.0
+
+
+def test_lookup_integer_coords_are_exact_gathers():
+    """wx = wy = 0 -> every output is exactly one pyramid value (or 0 outside)."""
+    f1, f2 = synthetic.synthetic_fmaps(1, 32, 16, 16, stream=9)
+    pyr = [p.to(DEV) for p in ocorr.corr_pyramid(f1, f2, 2)]
+    coords = ocorr.coords_grid(1, 16, 16).to(DEV)
+    out = _native.corr_lookup(pyr, coords, 2).cpu()
+    p0 = pyr[0].cpu().view(16, 16, 16, 16)
+    for q, (y, x) in enumerate([(0, 0), (7, 9), (15, 15)]):
+        for i in range(5):
+            for j in range(5):
+                yy, xx = y + j - 2, x + i - 2
+                exp = p0[y, x, yy, xx] if (0 <= yy < 16 and 0 <= xx < 16) else 0.0
+                assert out[0, i * 5 + j, y, x] == exp
+
+
+def test_lookup_non_finite_and_huge_coords_give_zero():
+    f1, f2 = synthetic.synthetic_fmaps(1, 16, 16, 16, stream=2)
+    pyr = [p.to(DEV) for p in ocorr.corr_pyramid(f1, f2, 4)]
+    coords = ocorr.coords_grid(1, 16, 16)
+    coords[0, 0, 0, 0] = float("nan")
+    coords[0, 1, 0, 1] = float("inf")
+    coords[0, 0, 0, 2] = 1e9
+    coords[0, 0, 0, 3] = -5e6
+    out = _native.corr_lookup(pyr, coords.to(DEV), 4).cpu()
+    assert torch.all(out[0, :, 0, :4] == 0)
+    assert torch.isfinite(out).all()
+
+
+def test_lookup_rejects_tiny_levels_q3():
+    f1, f2 = synthetic.synthetic_fmaps(1, 16, 8, 12, stream=2)
+    cb = CorrBlock(f1.to(DEV), f2.to(DEV))  # levels 8x12 .. 1x1
+    with pytest.raises(ValueError, match="2 pixels"):
+        cb(coords_grid(1, 8, 12, device=DEV))
+
+
+def test_lookup_full_size_spot_check():
+    """Config #2 shape (B=4, 128 x 128, C=256): spot-check 256 queries against the float64 oracle."""
+    b, h, w = 4, 128, 128
+    f1, f2 = synthetic.synthetic_fmaps(b, 256, h, w, stream=13)
+    cb = CorrBlock(f1.to(DEV), f2.to(DEV))
+    coords = coords_grid(b, h, w) + torch.from_numpy(synthetic.hash_normal(14, (b, 2, h, w), 4.0))
+    out = cb(coords.to(DEV)).cpu()
+    rng = np.random.default_rng(0)
+    qs = rng.integers(0, b * h * w, 256)
+    n = h * w
+    for q in qs:
+        bi, pix = divmod(int(q), n)
+        pyr = [cb.corr_pyramid[l][q : q + 1].cpu().numpy() for l in range(4)]
+        c = coords[bi : bi + 1, :, pix // w : pix // w + 1, pix % w : pix % w + 1].numpy()
+        ref = ocorr.corr_lookup_f64(pyr, c, 4)[0, :, 0, 0]
+        assert np.abs(out[bi, :, pix // w, pix % w].numpy() - ref).max() <= 1e-4
+
+
+# ----------------------------------------------------------------------------------------------------------
+# warp / grid_sample
+# ----------------------------------------------------------------------------------------------------------
+def test_warp_reference_unit_tests_exact():
+    """tests/operator/test_operator.py:6-38 of the reference, bit-exact."""
+    img = torch.tensor([[[1.0, 2.0]]]).unsqueeze(0).to(DEV)
+    flow = torch.tensor([[[1.0, 0.0]], [[0.0, 0.0]]]).unsqueeze(0).to(DEV)
+    assert torch.equal(optical_flow.warp(img, optical_flow.normalize(flow)).cpu(), torch.tensor([[[[2.0, 2.0]]]]))
+    img = torch.tensor([[[1.0], [2.0]]]).unsqueeze(0).to(DEV)
+    flow = torch.tensor([[[0.0], [0.0]], [[1.0], [0.0]]]).unsqueeze(0).to(DEV)
+    assert torch.equal(optical_flow.warp(img, optical_flow.normalize(flow)).cpu(), torch.tensor([[[[2.0], [2.0]]]]))
+
+
+def test_warp_matches_reference_goldens(golden):
+    g = golden("warp_small")
+    frame, flow = torch.from_numpy(g["frame"]).to(DEV), torch.from_numpy(g["flow"]).to(DEV)
+    for key in g:
+        if key.startswith("warp_") and key != "warp_default":
+            _, mode, pad, ac = key.split("_")
+            out = optical_flow.warp(frame, flow, mode, pad, bool(int(ac))).cpu().numpy()
+            err = np.abs(out - g[key]).max()
+            assert err <= 2e-3, (key, err)
+    assert np.abs(optical_flow.warp(frame, flow).cpu().numpy() - g["warp_default"]).max() <= 2e-3
+    fp = torch.from_numpy(g["flow_px"]).to(DEV)
+    out = optical_flow.integrate(fp, 0.5 * fp, -0.25 * fp).cpu().numpy()
+    assert np.abs(out - g["integrate_3"]).max() <= 2e-3
+
+
+@pytest.mark.parametrize("mode", ["bilinear", "nearest", "bicubic"])
+@pytest.mark.parametrize("pad", ["zeros", "border", "reflection"])
+@pytest.mark.parametrize("ac", [False, True])
+def test_warp_matches_oracle_sintel_frame(mode, pad, ac):
+    img0, _ = synthetic.synthetic_pair(2, 109, 256, seed=4)
+    flow = oop.normalize(torch.from_numpy(synthetic.hash_normal(6, (2, 2, 109, 256), 8.0)))
+    ref = oop.warp(img0, flow, mode, pad, ac)
+    got = optical_flow.warp(img0.to(DEV), flow.to(DEV), mode, pad, ac).cpu()
+    err = (got - ref).abs()
+    # nearest can flip a tap where the CPU and GPU grids differ by an ulp at a .5 boundary: allow a few
+    if mode == "nearest":
+        assert (err > 1e-3).float().mean().item() < 1e-3
+    else:
+        assert err.max().item() <= 2e-2 and err.mean().item() <= 1e-4
+
+
+def test_grid_sample_and_bilinear_sampler_match_oracle():
+    img = torch.from_numpy(synthetic.hash_normal(8, (6, 3, 20, 30), 1.0))
+    coords = torch.from_numpy(synthetic.hash_normal(9, (6, 7, 5, 2), 12.0)) + 12.0
+    ref = ocorr.bilinear_sampler(img, coords)
+    got = bilinear_sampler(img.to(DEV), coords.to(DEV)).cpu()
+    assert (got - ref).abs().max().item() <= 1e-5
+    out, mask = bilinear_sampler(img.to(DEV), coords.to(DEV), mask=True)
+    assert mask.shape == (6, 7, 5, 1)
+    grid = torch.from_numpy(synthetic.hash_normal(10, (2, 9, 11, 2), 0.8))
+    x = torch.from_numpy(synthetic.hash_normal(11, (2, 4, 13, 17), 1.0))
+    for mode in ("bilinear", "nearest", "bicubic"):
+        for pad in ("zeros", "border", "reflection"):
+            for ac in (False, True):
+                r = F.grid_sample(x, grid, mode=mode, padding_mode=pad, align_corners=ac)
+                gg = _native.grid_sample(x.to(DEV), grid.to(DEV), mode, pad, ac).cpu()
+                assert (gg - r).abs().max().item() <= 1e-4, (mode, pad, ac)
+
+
+def test_ops_follow_the_current_stream():
+    f1, f2 = synthetic.synthetic_fmaps(1, 256, 24, 32, stream=1)
+    s = torch.cuda.Stream()
+    with torch.cuda.stream(s):
+        cb = CorrBlock(f1.to(DEV), f2.to(DEV))
+        out = cb(coords_grid(1, 24, 32, device=DEV))
+    s.synchronize()
+    ref = ocorr.corr_lookup(ocorr.corr_pyramid(f1, f2, 4), ocorr.coords_grid(1, 24, 32), 4)
+    assert (out.cpu() - ref).abs().max().item() <= 1e-4

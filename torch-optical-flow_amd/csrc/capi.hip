@@ -1,0 +1,22 @@
+// Version / status entry points of liboflow_hip.so (include/oflow.h).
+#include "oflow_internal.h"
+
+extern "C" int oflow_abi_version(void) { return OFLOW_ABI_VERSION; }
+
+extern "C" const char* oflow_status_string(int status) {
+  switch (status) {
+    case OFLOW_OK: return "ok";
+    case OFLOW_E_NULL: return "null pointer argument";
+    case OFLOW_E_SHAPE: return "invalid or inconsistent size";
+    case OFLOW_E_LEVELS: return "num_levels outside [1, 8]";
+    case OFLOW_E_TINY:
+      return "a correlation pyramid level is smaller than 2 pixels in H or W (the reference divides by "
+             "W_l-1 / H_l-1 there and returns NaN); pad the input images to at least 128x128";
+    case OFLOW_E_RADIUS: return "radius outside [0, 7]";
+    case OFLOW_E_MODE: return "unknown interpolation or padding mode";
+    case OFLOW_E_ALIGN: return "device pointer is not 4-byte aligned";
+    default:
+      if (status > 0) return hipGetErrorString(static_cast<hipError_t>(status));
+      return "unknown oflow status";
+  }
+}

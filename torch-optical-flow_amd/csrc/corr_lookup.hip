@@ -1,0 +1,180 @@
+// Multi-level windowed bilinear lookup into the correlation pyramid (gfx950).
+//
+// Replaces methods/raft/model/corr.py:56-77 (CorrBlock.__call__) and utils.py:64-80 (bilinear_sampler ->
+// F.grid_sample(align_corners=True, padding_mode='zeros')), including the window channel order of the
+// reference (Q1): channel l*(2r+1)^2 + i*(2r+1) + j samples (x/2^l + i - r, y/2^l + j - r).
+//
+// Pixel-space formulation: for one (query, level) every window tap shares the fractional
+// offset (wx, wy) of the centre, so the lookup is a (2r+2)^2 patch gather plus one fixed 2x2 stencil. The
+// normalise -> unnormalise round trip of the reference (x -> 2x/(W-1)-1 -> x) is skipped; it only adds
+// ulp-level noise (<= 2.2e-5 abs measured).
+//
+// Workgroup = 64 queries x 1 level, 256 threads:
+//   phase 0: 64 lanes decode the query centres (floor, weights, output offsets) into LDS;
+//   phase 1: all 256 threads gather the 64 patches (consecutive threads read consecutive columns of one
+//            patch row: each wave instruction touches ~6 row segments) into LDS, stride (2r+2)^2+1 floats
+//            (odd: the compute phase's per-query reads are bank-conflict free);
+//   phase 2: each thread emits outputs channel-major so that 64 consecutive lanes write 64 consecutive
+//            query pixels of one output channel (256-B coalesced stores of the NCHW output).
+#include "oflow_internal.h"
+
+namespace oflow {
+namespace {
+
+constexpr int kQ = 64;  // queries per workgroup
+constexpr int kThreads = 256;
+
+struct LookupArgs {
+  const float* lv[OFLOW_MAX_LEVELS];
+  int Hl[OFLOW_MAX_LEVELS];
+  int Wl[OFLOW_MAX_LEVELS];
+  const float* coords;  // (B, 2, N)
+  float* out;           // (B, nlev*K*K, N)
+  int N;                // query pixels per batch element
+  int total;            // B * N
+  int cout;             // nlev * K * K
+};
+
+template <int R>
+__global__ __launch_bounds__(kThreads) void corr_lookup_kernel(LookupArgs a) {
+  constexpr int PK = 2 * R + 2;   // patch side
+  constexpr int K = 2 * R + 1;    // window side
+  constexpr int PS = PK * PK;     // patch size
+  constexpr int QS = PS + 1;      // LDS stride per query (odd)
+  constexpr int ITEMS = kQ * PS;
+  constexpr int PER = (ITEMS + kThreads - 1) / kThreads;
+  constexpr int OUTS = kQ * K * K;
+  constexpr int PERO = (OUTS + kThreads - 1) / kThreads;
+
+  __shared__ float sP[kQ * QS];
+  __shared__ int sX[kQ], sY[kQ];
+  __shared__ float4 sW[kQ];
+  __shared__ long long sO[kQ];
+
+  const int lvl = blockIdx.y;
+  const int q0 = blockIdx.x * kQ;
+  const int Hl = a.Hl[lvl], Wl = a.Wl[lvl];
+  const float* __restrict__ L = a.lv[lvl];
+  const float inv = 1.0f / static_cast<float>(1 << lvl);  // exact power of two (corr.py:68)
+
+  if (threadIdx.x < kQ) {
+    const int q = q0 + threadIdx.x;
+    int xs = -(1 << 28), ys = -(1 << 28);
+    float4 w = make_float4(0.f, 0.f, 0.f, 0.f);
+    long long off = -1;
+    if (q < a.total) {
+      const int b = q / a.N;
+      const int pix = q - b * a.N;
+      const float cx = a.coords[(size_t)(2 * b) * a.N + pix] * inv;
+      const float cy = a.coords[(size_t)(2 * b + 1) * a.N + pix] * inv;
+      // |c| >= 2^22 (or NaN/inf) puts every tap far outside any level: all-zero window.
+      if (fabsf(cx) < 4194304.0f && fabsf(cy) < 4194304.0f) {
+        const float fx = floorf(cx), fy = floorf(cy);
+        const float wx = cx - fx, wy = cy - fy;  // exact
+        const float ex = 1.0f - wx, ey = 1.0f - wy;
+        xs = static_cast<int>(fx) - R;
+        ys = static_cast<int>(fy) - R;
+        w = make_float4(ey * ex, ey * wx, wy * ex, wy * wx);  // nw, ne, sw, se (grid_sample CPU weights)
+      }
+      off = (long long)b * a.cout * a.N + (long long)lvl * K * K * a.N + pix;
+    }
+    sX[threadIdx.x] = xs;
+    sY[threadIdx.x] = ys;
+    sW[threadIdx.x] = w;
+    sO[threadIdx.x] = off;
+  }
+  __syncthreads();
+
+  float v[PER];
+#pragma unroll
+  for (int s = 0; s < PER; ++s) {
+    const int item = threadIdx.x + kThreads * s;
+    v[s] = 0.0f;
+    if (item < ITEMS) {
+      const int q = item / PS;
+      const int rem = item - q * PS;
+      const int row = rem / PK;
+      const int col = rem - row * PK;
+      const int y = sY[q] + row, x = sX[q] + col;
+      if (q0 + q < a.total && static_cast<unsigned>(y) < static_cast<unsigned>(Hl) &&
+          static_cast<unsigned>(x) < static_cast<unsigned>(Wl))
+        v[s] = L[(size_t)(q0 + q) * (size_t)Hl * Wl + (size_t)y * Wl + x];
+    }
+  }
+#pragma unroll
+  for (int s = 0; s < PER; ++s) {
+    const int item = threadIdx.x + kThreads * s;
+    if (item < ITEMS) {
+      const int q = item / PS;
+      sP[q * QS + (item - q * PS)] = v[s];
+    }
+  }
+  __syncthreads();
+
+#pragma unroll
+  for (int s = 0; s < PERO; ++s) {
+    const int o = threadIdx.x + kThreads * s;
+    if (o < OUTS) {
+      const int c = o / kQ;
+      const int q = o - c * kQ;
+      const long long off = sO[q];
+      if (off >= 0) {
+        const int i = c / K;           // moves x
+        const int j = c - i * K;       // moves y
+        const float* p = &sP[q * QS + j * PK + i];
+        const float4 w = sW[q];
+        const float val = p[0] * w.x + p[1] * w.y + p[PK] * w.z + p[PK + 1] * w.w;
+        a.out[off + (long long)c * a.N] = val;
+      }
+    }
+  }
+}
+
+template <int R>
+int launch_lookup(const LookupArgs& a, int nlev, hipStream_t s) {
+  dim3 grid((a.total + kQ - 1) / kQ, nlev);
+  hipLaunchKernelGGL(corr_lookup_kernel<R>, grid, dim3(kThreads), 0, s, a);
+  return launch_status();
+}
+
+}  // namespace
+}  // namespace oflow
+
+using namespace oflow;
+
+extern "C" int oflow_corr_lookup_f32(const float* const* d_levels, const int* level_h, const int* level_w,
+                                     int num_levels, const float* d_coords, int B, int H, int W, int radius,
+                                     float* d_out, void* stream) {
+  if (!d_levels || !level_h || !level_w || !d_coords || !d_out) return OFLOW_E_NULL;
+  if (B <= 0 || H <= 0 || W <= 0) return OFLOW_E_SHAPE;
+  if (num_levels < 1 || num_levels > OFLOW_MAX_LEVELS) return OFLOW_E_LEVELS;
+  if (radius < 0 || radius > OFLOW_MAX_RADIUS) return OFLOW_E_RADIUS;
+  if ((long long)B * H * W >= (1ll << 31) / 64) return OFLOW_E_SHAPE;
+  LookupArgs a{};
+  for (int l = 0; l < num_levels; ++l) {
+    if (!d_levels[l]) return OFLOW_E_NULL;
+    // the reference normalises by (W_l - 1), (H_l - 1): a level under 2 px gives inf/NaN there (Q3)
+    if (level_h[l] < 2 || level_w[l] < 2) return OFLOW_E_TINY;
+    a.lv[l] = d_levels[l];
+    a.Hl[l] = level_h[l];
+    a.Wl[l] = level_w[l];
+  }
+  const int K = 2 * radius + 1;
+  a.coords = d_coords;
+  a.out = d_out;
+  a.N = H * W;
+  a.total = B * H * W;
+  a.cout = num_levels * K * K;
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  switch (radius) {
+    case 0: return launch_lookup<0>(a, num_levels, s);
+    case 1: return launch_lookup<1>(a, num_levels, s);
+    case 2: return launch_lookup<2>(a, num_levels, s);
+    case 3: return launch_lookup<3>(a, num_levels, s);
+    case 4: return launch_lookup<4>(a, num_levels, s);
+    case 5: return launch_lookup<5>(a, num_levels, s);
+    case 6: return launch_lookup<6>(a, num_levels, s);
+    case 7: return launch_lookup<7>(a, num_levels, s);
+    default: return OFLOW_E_RADIUS;
+  }
+}

@@ -1,0 +1,214 @@
+// Inverse warp by a flow field = F.grid_sample(frame, linspace-grid + flow) (gfx950).
+//
+// Replaces optical_flow/operator/operator.py:8-56 (warp -> warp_grid -> grid_sample). The base grid is
+// torch.linspace(-1, 1, n) evaluated in fp32 with ATen's two-sided formula (start + step*i below the halfway
+// index, end - step*(n-1-i) from it), flow is already in normalized units, and every grid_sample mode is
+// implemented with the CPU kernel's arithmetic forms (unnormalize (g+1)*((n-1)/2) or (g+1)*(n/2)-0.5,
+// e = 1-w weights, A = -0.75 cubic), so the result tracks the reference PyTorch-CPU path to ulp-level noise:
+//   mode: bilinear | nearest (round half to even) | bicubic;  padding: zeros | border | reflection.
+// One thread per output pixel: flow read and output writes are coalesced along W; the gathered frame taps of
+// neighbouring lanes are neighbours too for smooth flow, so they hit the same cache lines.
+#include "oflow_internal.h"
+
+#pragma clang fp contract(off)
+
+namespace oflow {
+namespace {
+
+struct WarpArgs {
+  const float* frame;  // (B, C, H, W)
+  const float* flow;   // FLOW: (B, 2, Ho, Wo) normalized flow; else the grid (B, Ho, Wo, 2)
+  float* out;          // (B, C, Ho, Wo)
+  int B, C, H, W;      // input sizes
+  int Ho, Wo;          // output sizes (== H, W for warp)
+  int pad;
+  int ac;
+};
+
+__device__ __forceinline__ float linspace_m1_p1(int i, int n) {
+  if (n == 1) return -1.0f;
+  const float step = 2.0f / static_cast<float>(n - 1);
+  return i < n / 2 ? -1.0f + step * static_cast<float>(i) : 1.0f - step * static_cast<float>(n - 1 - i);
+}
+
+__device__ __forceinline__ float unnormalize(float g, int n, int ac) {
+  return ac ? (g + 1.0f) * (static_cast<float>(n - 1) / 2.0f) : (g + 1.0f) * (static_cast<float>(n) / 2.0f) - 0.5f;
+}
+
+__device__ __forceinline__ float clip(float x, int n) { return fminf(static_cast<float>(n - 1), fmaxf(x, 0.0f)); }
+
+__device__ __forceinline__ float reflect(float x, int twice_low, int twice_high) {
+  if (twice_low == twice_high) return 0.0f;
+  const float mn = static_cast<float>(twice_low) / 2.0f;
+  const float span = static_cast<float>(twice_high - twice_low) / 2.0f;
+  x = fabsf(x - mn);
+  const float extra = fmodf(x, span);
+  const int flips = static_cast<int>(floorf(x / span));
+  return (flips % 2 == 0) ? extra + mn : span - extra + mn;
+}
+
+// padding applied to an unnormalized coordinate (ATen compute_coordinates)
+__device__ __forceinline__ float pad_coord(float x, int n, int pad, int ac) {
+  if (pad == OFLOW_PAD_BORDER) {
+    x = clip(x, n);
+  } else if (pad == OFLOW_PAD_REFLECTION) {
+    x = ac ? reflect(x, 0, 2 * (n - 1)) : reflect(x, -1, 2 * n - 1);
+    x = clip(x, n);
+  }
+  return x;
+}
+
+// keeps float->int conversion defined for huge / non-finite coordinates (those taps are out of bounds)
+__device__ __forceinline__ int to_index(float x) {
+  return (x > -1048576.0f && x < 1048576.0f) ? static_cast<int>(x) : -1048576;
+}
+
+__device__ __forceinline__ bool inb(int x, int y, int W, int H) {
+  return static_cast<unsigned>(x) < static_cast<unsigned>(W) && static_cast<unsigned>(y) < static_cast<unsigned>(H);
+}
+
+__device__ __forceinline__ void cubic_coeffs(float t, float c[4]) {
+  const float A = -0.75f;
+  float x = t + 1.0f;
+  c[0] = ((A * x - 5.0f * A) * x + 8.0f * A) * x - 4.0f * A;
+  x = t;
+  c[1] = ((A + 2.0f) * x - (A + 3.0f)) * x * x + 1.0f;
+  x = 1.0f - t;
+  c[2] = ((A + 2.0f) * x - (A + 3.0f)) * x * x + 1.0f;
+  x = 2.0f - t;
+  c[3] = ((A * x - 5.0f * A) * x + 8.0f * A) * x - 4.0f * A;
+}
+
+template <int MODE, bool FLOW>
+__global__ __launch_bounds__(256) void grid_warp_kernel(WarpArgs a) {
+  const int HW = a.H * a.W;
+  const int HWo = a.Ho * a.Wo;
+  const long long total = (long long)a.B * HWo;
+  for (long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x; t < total;
+       t += (long long)gridDim.x * blockDim.x) {
+    const int b = static_cast<int>(t / HWo);
+    const int pix = static_cast<int>(t - (long long)b * HWo);
+    float gx, gy;
+    if constexpr (FLOW) {  // warp_grid fused: linspace base grid + normalized flow (operator.py:49-55)
+      const int y = pix / a.Wo, x = pix - y * a.Wo;
+      gx = linspace_m1_p1(x, a.Wo) + a.flow[(size_t)(2 * b) * HWo + pix];
+      gy = linspace_m1_p1(y, a.Ho) + a.flow[(size_t)(2 * b + 1) * HWo + pix];
+    } else {
+      const float2 g = *reinterpret_cast<const float2*>(a.flow + 2 * ((size_t)b * HWo + pix));
+      gx = g.x;
+      gy = g.y;
+    }
+    const float* src = a.frame + (size_t)b * a.C * HW;
+    float* dst = a.out + (size_t)b * a.C * HWo + pix;
+
+    if constexpr (MODE == OFLOW_INTERP_BICUBIC) {
+      const float ix = unnormalize(gx, a.W, a.ac), iy = unnormalize(gy, a.H, a.ac);
+      const float fx = floorf(ix), fy = floorf(iy);
+      float cx[4], cy[4];
+      cubic_coeffs(ix - fx, cx);
+      cubic_coeffs(iy - fy, cy);
+      int xi[4], yi[4];
+      bool xv[4], yv[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const float px = pad_coord(fx - 1.0f + k, a.W, a.pad, a.ac);
+        const float py = pad_coord(fy - 1.0f + k, a.H, a.pad, a.ac);
+        xi[k] = to_index(px);
+        yi[k] = to_index(py);
+        xv[k] = static_cast<unsigned>(xi[k]) < static_cast<unsigned>(a.W);
+        yv[k] = static_cast<unsigned>(yi[k]) < static_cast<unsigned>(a.H);
+      }
+      for (int c = 0; c < a.C; ++c) {
+        const float* s = src + (size_t)c * HW;
+        float acc = 0.0f;
+        float rows[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          float r = 0.0f;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const float v = (xv[j] && yv[i]) ? s[yi[i] * a.W + xi[j]] : 0.0f;
+            r = j == 0 ? v * cx[0] : r + v * cx[j];
+          }
+          rows[i] = r;
+        }
+        acc = rows[0] * cy[0] + rows[1] * cy[1] + rows[2] * cy[2] + rows[3] * cy[3];
+        dst[(size_t)c * HWo] = acc;
+      }
+    } else {
+      const float ix = pad_coord(unnormalize(gx, a.W, a.ac), a.W, a.pad, a.ac);
+      const float iy = pad_coord(unnormalize(gy, a.H, a.ac), a.H, a.pad, a.ac);
+      if constexpr (MODE == OFLOW_INTERP_NEAREST) {
+        const int xn = to_index(rintf(ix)), yn = to_index(rintf(iy));
+        const bool ok = inb(xn, yn, a.W, a.H);
+        for (int c = 0; c < a.C; ++c) dst[(size_t)c * HWo] = ok ? src[(size_t)c * HW + yn * a.W + xn] : 0.0f;
+      } else {
+        const float fx = floorf(ix), fy = floorf(iy);
+        const int x0 = to_index(fx), y0 = to_index(fy);
+        const float wx = ix - fx, wy = iy - fy;
+        const float ex = 1.0f - wx, ey = 1.0f - wy;
+        const float nw = ey * ex, ne = ey * wx, sw = wy * ex, se = wy * wx;
+        const bool bnw = inb(x0, y0, a.W, a.H), bne = inb(x0 + 1, y0, a.W, a.H);
+        const bool bsw = inb(x0, y0 + 1, a.W, a.H), bse = inb(x0 + 1, y0 + 1, a.W, a.H);
+        for (int c = 0; c < a.C; ++c) {
+          const float* s = src + (size_t)c * HW;
+          const float vnw = bnw ? s[y0 * a.W + x0] : 0.0f;
+          const float vne = bne ? s[y0 * a.W + x0 + 1] : 0.0f;
+          const float vsw = bsw ? s[(y0 + 1) * a.W + x0] : 0.0f;
+          const float vse = bse ? s[(y0 + 1) * a.W + x0 + 1] : 0.0f;
+          dst[(size_t)c * HWo] = vnw * nw + vne * ne + vsw * sw + vse * se;
+        }
+      }
+    }
+  }
+}
+
+}  // namespace
+}  // namespace oflow
+
+using namespace oflow;
+
+namespace {
+template <bool FLOW>
+int launch_warp(const WarpArgs& a, int mode, hipStream_t s) {
+  const long long total = (long long)a.B * a.Ho * a.Wo;
+  const long long want = (total + 255) / 256;
+  dim3 grid(static_cast<unsigned>(want < 65535 ? want : 65535));
+  switch (mode) {
+    case OFLOW_INTERP_BILINEAR:
+      hipLaunchKernelGGL((grid_warp_kernel<OFLOW_INTERP_BILINEAR, FLOW>), grid, dim3(256), 0, s, a);
+      break;
+    case OFLOW_INTERP_NEAREST:
+      hipLaunchKernelGGL((grid_warp_kernel<OFLOW_INTERP_NEAREST, FLOW>), grid, dim3(256), 0, s, a);
+      break;
+    case OFLOW_INTERP_BICUBIC:
+      hipLaunchKernelGGL((grid_warp_kernel<OFLOW_INTERP_BICUBIC, FLOW>), grid, dim3(256), 0, s, a);
+      break;
+    default:
+      return OFLOW_E_MODE;
+  }
+  return launch_status();
+}
+}  // namespace
+
+extern "C" int oflow_grid_warp_f32(const float* d_frame, const float* d_flow, int B, int C, int H, int W, int mode,
+                                   int padding_mode, int align_corners, float* d_out, void* stream) {
+  if (!d_frame || !d_flow || !d_out) return OFLOW_E_NULL;
+  if (B <= 0 || C <= 0 || H <= 0 || W <= 0) return OFLOW_E_SHAPE;
+  if ((long long)C * H * W >= (1ll << 31) || (long long)B * H * W >= (1ll << 40)) return OFLOW_E_SHAPE;
+  if (padding_mode < OFLOW_PAD_ZEROS || padding_mode > OFLOW_PAD_REFLECTION) return OFLOW_E_MODE;
+  WarpArgs a{d_frame, d_flow, d_out, B, C, H, W, H, W, padding_mode, align_corners ? 1 : 0};
+  return launch_warp<true>(a, mode, static_cast<hipStream_t>(stream));
+}
+
+extern "C" int oflow_grid_sample_f32(const float* d_input, const float* d_grid, int B, int C, int H, int W, int Ho,
+                                     int Wo, int mode, int padding_mode, int align_corners, float* d_out,
+                                     void* stream) {
+  if (!d_input || !d_grid || !d_out) return OFLOW_E_NULL;
+  if (B <= 0 || C <= 0 || H <= 0 || W <= 0 || Ho <= 0 || Wo <= 0) return OFLOW_E_SHAPE;
+  if ((long long)C * H * W >= (1ll << 31) || (long long)C * Ho * Wo >= (1ll << 31)) return OFLOW_E_SHAPE;
+  if ((reinterpret_cast<uintptr_t>(d_grid) & 7) != 0) return OFLOW_E_ALIGN;
+  if (padding_mode < OFLOW_PAD_ZEROS || padding_mode > OFLOW_PAD_REFLECTION) return OFLOW_E_MODE;
+  WarpArgs a{d_input, d_grid, d_out, B, C, H, W, Ho, Wo, padding_mode, align_corners ? 1 : 0};
+  return launch_warp<false>(a, mode, static_cast<hipStream_t>(stream));
+}

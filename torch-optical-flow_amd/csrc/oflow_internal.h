@@ -1,0 +1,35 @@
+// Internal helpers shared by the liboflow_hip kernels (gfx950 / CDNA4 only).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "oflow.h"
+
+namespace oflow {
+
+// Lane exchange inside 4-lane quads via DPP (no LDS traffic): quad_perm [1,0,3,2] and [2,3,0,1].
+__device__ __forceinline__ float dpp_xor1(float v) {
+  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0xB1, 0xF, 0xF, false));
+}
+__device__ __forceinline__ float dpp_xor2(float v) {
+  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x4E, 0xF, 0xF, false));
+}
+// xor-4 within 32-lane groups: ds_swizzle bit mode (and 0x1F, or 0, xor 4); crossbar only, no LDS memory.
+__device__ __forceinline__ float swz_xor4(float v) {
+  return __int_as_float(__builtin_amdgcn_ds_swizzle(__float_as_int(v), 0x1F | (4 << 10)));
+}
+
+// avg_pool2d(2, stride=2) of one output: ATen sums the 2x2 window row by row into a zero-initialised
+// accumulator and divides by 4 (exact), i.e. (((a + b) + c) + d) / 4 with a,b the upper pair.
+__device__ __forceinline__ float pool4(float a, float b, float c, float d) {
+  float s = __fadd_rn(__fadd_rn(__fadd_rn(a, b), c), d);
+  return s * 0.25f;
+}
+
+inline int launch_status() {
+  hipError_t e = hipGetLastError();
+  return e == hipSuccess ? OFLOW_OK : static_cast<int>(e);
+}
+
+}  // namespace oflow

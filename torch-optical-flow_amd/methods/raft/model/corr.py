@@ -1,0 +1,34 @@
+"""``CorrBlock`` drop-in (reference: methods/raft/model/corr.py:37-87) on the gfx950 kernels.
+
+* ``__init__`` — one launch of ``oflow_corr_pyramid_f32``: fp32 MFMA all-pairs volume with the 1/sqrt(C) scale
+  and the floor 2x2 average-pool levels fused into the GEMM epilogue (`corr.py:38-54, 79-87`).
+* ``__call__`` — one launch of ``oflow_corr_lookup_f32`` for all levels: the (2r+1)^2 bilinear window per level,
+  written straight into the (B, L*(2r+1)^2, H, W) fp32 NCHW output (`corr.py:56-77`, `utils.py:64-80`).
+
+Attributes match the reference: ``num_levels``, ``radius`` and ``corr_pyramid`` (list of (B*H*W, 1, H_l, W_l)
+fp32 tensors; here views of one allocation). Divergence (documented): where a level is under 2 px in
+H or W the reference returns NaN (it divides by W_l-1); this build raises ``ValueError`` at lookup time.
+"""
+from __future__ import annotations
+
+from typing import List
+
+from torch import Tensor
+
+from optical_flow import _native
+
+
+class CorrBlock:
+    def __init__(self, fmap1: Tensor, fmap2: Tensor, num_levels: int = 4, radius: int = 4) -> None:
+        self.num_levels = num_levels
+        self.radius = radius
+        self.corr_pyramid: List[Tensor] = _native.corr_pyramid(fmap1, fmap2, num_levels)
+
+    def __call__(self, coords: Tensor) -> Tensor:
+        return _native.corr_lookup(self.corr_pyramid, coords, self.radius)
+
+    @staticmethod
+    def corr(fmap1: Tensor, fmap2: Tensor) -> Tensor:
+        """All-pairs volume (B, H, W, 1, H, W) / sqrt(C) (`corr.py:79-87`)."""
+        b, _, h, w = fmap1.shape
+        return _native.corr_pyramid(fmap1, fmap2, 1)[0].view(b, h, w, 1, h, w)

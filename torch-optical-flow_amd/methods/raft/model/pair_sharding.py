@@ -1,0 +1,106 @@
+"""Image-pair batch sharding over one process per GPU (``torch.distributed``; backend "nccl" = RCCL on ROCm).
+
+Every image pair is an independent RAFT forward (no cross-pair state; cnet BatchNorm uses running statistics
+in eval mode), so the only communication is at the edges of the batch:
+  * ``scatter_pairs``: rank ``src`` holds the global (B, 3, H, W) pair batch and scatters contiguous shards,
+    one per rank (RCCL lowers scatter to per-peer sends: each peer receives over its own xGMI link);
+  * ``gather_flows``:  shards' flows go back to rank ``dst``.
+There is no per-iteration exchange. Ragged batches (B % world_size != 0) are padded to equal chunks for the
+collective and trimmed on both sides. The same code runs on gloo with CPU tensors (tests).
+"""
+from __future__ import annotations
+
+from typing import Callable, Optional, Sequence, Tuple
+
+import torch
+import torch.distributed as dist
+from torch import Tensor
+
+
+def shard_bounds(global_batch: int, world_size: int, rank: int) -> Tuple[int, int]:
+    """[start, stop) of ``rank``'s contiguous shard; shards differ in size by at most one pair."""
+    base, extra = divmod(global_batch, world_size)
+    start = rank * base + min(rank, extra)
+    return start, start + base + (1 if rank < extra else 0)
+
+
+def _world(group) -> Tuple[int, int]:
+    return dist.get_world_size(group), dist.get_rank(group)
+
+
+def _meta(t: Optional[Tensor], src: int, group, device: torch.device) -> Sequence[int]:
+    rank = dist.get_rank(group)
+    meta = torch.zeros(5, dtype=torch.int64, device=device)
+    if rank == src:
+        meta[: t.dim()] = torch.tensor(t.shape, dtype=torch.int64)
+    dist.broadcast(meta, src=dist.get_global_rank(group, src) if group is not None else src, group=group)
+    return [int(v) for v in meta.tolist() if v != 0] if rank != src else list(t.shape)
+
+
+def scatter_pairs(
+    image0: Optional[Tensor],
+    image1: Optional[Tensor],
+    device: torch.device,
+    src: int = 0,
+    group=None,
+) -> Tuple[Tensor, Tensor]:
+    """Scatter the pair batch held by rank ``src`` (other ranks pass ``None``); returns this rank's shard."""
+    world, rank = _world(group)
+    shape = _meta(image0, src, group, device)
+    b, rest = shape[0], shape[1:]
+    chunk = -(-b // world)
+    start, stop = shard_bounds(b, world, rank)
+    outs = []
+    for img in (image0, image1):
+        recv = torch.empty([chunk] + rest, dtype=torch.float32, device=device)
+        scatter_list = None
+        if rank == src:
+            img = img.to(device=device, dtype=torch.float32)
+            scatter_list = []
+            for r in range(world):
+                s0, s1 = shard_bounds(b, world, r)
+                piece = img[s0:s1]
+                if s1 - s0 < chunk:
+                    piece = torch.cat([piece, piece.new_zeros([chunk - (s1 - s0)] + rest)], dim=0)
+                scatter_list.append(piece.contiguous())
+        dist.scatter(recv, scatter_list, src=dist.get_global_rank(group, src) if group is not None else src, group=group)
+        outs.append(recv[: stop - start])
+    return outs[0], outs[1]
+
+
+def gather_flows(flow: Tensor, global_batch: int, dst: int = 0, group=None) -> Optional[Tensor]:
+    """Gather every rank's (b_r, ...) flow shard to rank ``dst``; returns the (B, ...) batch there, else None."""
+    world, rank = _world(group)
+    chunk = -(-global_batch // world)
+    rest = list(flow.shape[1:])
+    send = flow
+    if flow.shape[0] < chunk:
+        send = torch.cat([flow, flow.new_zeros([chunk - flow.shape[0]] + rest)], dim=0)
+    send = send.contiguous()
+    gather_list = [torch.empty_like(send) for _ in range(world)] if rank == dst else None
+    dist.gather(send, gather_list, dst=dist.get_global_rank(group, dst) if group is not None else dst, group=group)
+    if rank != dst:
+        return None
+    parts = []
+    for r in range(world):
+        s0, s1 = shard_bounds(global_batch, world, r)
+        parts.append(gather_list[r][: s1 - s0])
+    return torch.cat(parts, dim=0)
+
+
+def infer_sharded(
+    forward: Callable[[Tensor, Tensor], Tuple[Tensor, Tensor]],
+    image0: Optional[Tensor],
+    image1: Optional[Tensor],
+    device: torch.device,
+    src: int = 0,
+    group=None,
+) -> Tuple[Optional[Tensor], Optional[Tensor]]:
+    """scatter -> ``forward(shard0, shard1) -> (flow_low, flow_up)`` on every rank -> gather to ``src``."""
+    s0, s1 = scatter_pairs(image0, image1, device, src=src, group=group)
+    world, _ = _world(group)
+    global_batch = image0.shape[0] if dist.get_rank(group) == src else None
+    gb = torch.tensor([global_batch or 0], dtype=torch.int64, device=device)
+    dist.broadcast(gb, src=dist.get_global_rank(group, src) if group is not None else src, group=group)
+    low, up = forward(s0, s1)
+    return gather_flows(low, int(gb.item()), dst=src, group=group), gather_flows(up, int(gb.item()), dst=src, group=group)

@@ -1,0 +1,161 @@
+"""RAFT inference model (reference: methods/raft/model/raft.py:21-147), MI355X-native correlation path.
+
+Same constructor arguments, ``hparams`` attribute, sub-modules and ``state_dict`` keys as the reference's
+LightningModule, so its checkpoints load unchanged; the training loop (`raft.py:149-260`: loss, optimizers,
+W&B logging) is out of scope. ``forward`` keeps the reference's semantics and return
+values; three output-identical changes remove host work from the loop:
+  * the correlation pyramid and every lookup run on the gfx950 kernels (``model.corr.CorrBlock``);
+  * coordinate grids are built on the device (no CPU build + H2D copy, `raft.py:68-69`);
+  * with ``test_mode=True`` only the last iteration's convex upsampling is computed — the reference computes
+    all ``iters`` and returns only the last (Q11, `raft.py:136-145`).
+"""
+from __future__ import annotations
+
+import os
+from typing import Any, Dict, List, Optional, Tuple, Union
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+from torch import Tensor
+
+from .corr import CorrBlock
+from .extractor import BasicEncoder
+from .update import BasicUpdateBlock
+from .utils import coords_grid, upflow8
+
+
+class HParams(dict):
+    """Attribute access to the constructor arguments (Lightning's ``self.hparams`` as used in `raft.py`)."""
+
+    def __getattr__(self, key: str) -> Any:
+        try:
+            return self[key]
+        except KeyError as e:
+            raise AttributeError(key) from e
+
+
+def strip_module(state_dict: Dict[str, Tensor]) -> Dict[str, Tensor]:
+    """Drop the ``module.`` prefix of DataParallel checkpoints (reference `pretrained/convert.py:4-11`)."""
+    return {(k[7:] if k.startswith("module.") else k): v for k, v in state_dict.items()}
+
+
+class RAFT(nn.Module):
+    def __init__(
+        self,
+        hidden_dim: int = 128,
+        context_dim: int = 128,
+        corr_levels: int = 4,
+        corr_radius: int = 4,
+        iters: int = 12,
+        iters_val: int = 24,
+        gamma: float = 0.8,
+        dropout: float = 0.0,
+        lr: float = 0.00002,
+        wdecay: float = 0.00005,
+        epsilon: float = 1e-8,
+    ) -> None:
+        super().__init__()
+        self.hparams = HParams(
+            hidden_dim=hidden_dim,
+            context_dim=context_dim,
+            corr_levels=corr_levels,
+            corr_radius=corr_radius,
+            iters=iters,
+            iters_val=iters_val,
+            gamma=gamma,
+            dropout=dropout,
+            lr=lr,
+            wdecay=wdecay,
+            epsilon=epsilon,
+        )
+        self.fnet = BasicEncoder(output_dim=256, norm_fn="instance", dropout=dropout)
+        self.cnet = BasicEncoder(output_dim=hidden_dim + context_dim, norm_fn="batch", dropout=dropout)
+        self.update_block = BasicUpdateBlock(corr_levels=corr_levels, corr_radius=corr_radius, hidden_dim=hidden_dim)
+
+    # -- checkpoints -------------------------------------------------------------------------------------
+    @classmethod
+    def load_from_checkpoint(cls, checkpoint_path: Union[str, os.PathLike], map_location=None, **kwargs) -> "RAFT":
+        """Load a Lightning ``.ckpt`` (``state_dict`` + ``hyper_parameters``) or an official ``.pth``
+        (``module.``-prefixed keys) with ``torch.load(weights_only=True)``."""
+        ckpt = torch.load(checkpoint_path, map_location=map_location or "cpu", weights_only=True)
+        hp = {}
+        if isinstance(ckpt, dict) and "state_dict" in ckpt:
+            hp = dict(ckpt.get("hyper_parameters", {}) or {})
+            sd = ckpt["state_dict"]
+        else:
+            sd = ckpt
+        hp.update(kwargs)
+        model = cls(**{k: v for k, v in hp.items() if k in cls.__init__.__code__.co_varnames})
+        sd = {k: v for k, v in strip_module(sd).items() if not k.startswith(("epe_", "f1_"))}
+        model.load_state_dict(sd)
+        return model
+
+    def freeze_bn(self) -> None:
+        for m in self.modules():
+            if isinstance(m, nn.BatchNorm2d):
+                m.eval()
+
+    # -- forward -----------------------------------------------------------------------------------------
+    @staticmethod
+    def initialize_flow(img: Tensor) -> Tuple[Tensor, Tensor]:
+        """coords0 = coords1 = pixel grid at 1/8 resolution; flow = coords1 - coords0 (`raft.py:64-71`)."""
+        n, _, h, w = img.shape
+        coords0 = coords_grid(n, h // 8, w // 8, device=img.device)
+        return coords0, coords0.clone()
+
+    @staticmethod
+    def upsample_flow(flow: Tensor, mask: Tensor) -> Tensor:
+        """[H/8, W/8, 2] -> [H, W, 2] by a softmax-weighted 3x3 convex combination (`raft.py:73-85`)."""
+        n, _, h, w = flow.shape
+        mask = torch.softmax(mask.view(n, 1, 9, 8, 8, h, w), dim=2)
+        up_flow = F.unfold(8 * flow, [3, 3], padding=1).view(n, 2, 9, 1, 1, h, w)
+        up_flow = torch.sum(mask * up_flow, dim=2).permute(0, 1, 4, 2, 5, 3)
+        return up_flow.reshape(n, 2, 8 * h, 8 * w)
+
+    def forward(
+        self,
+        image0: Tensor,
+        image1: Tensor,
+        iters: int = 12,
+        flow_init: Optional[Tensor] = None,
+        upsample: bool = True,
+        test_mode: bool = False,
+    ) -> Union[Tensor, Tuple[Tensor, Tensor], List[Tensor]]:
+        """Estimate optical flow between pairs of frames (`raft.py:87-147`). Images (B, 3, H, W) in [0, 255]
+        with H, W divisible by 8 (use ``InputPadder``). Returns ``(coords1 - coords0, flow_up)`` in test mode,
+        else the list of ``iters`` upsampled predictions."""
+        image0 = (2 * (image0 / 255.0) - 1.0).contiguous()
+        image1 = (2 * (image1 / 255.0) - 1.0).contiguous()
+        hdim, cdim = self.hparams.hidden_dim, self.hparams.context_dim
+
+        fmap1, fmap2 = self.fnet([image0, image1])
+        corr_fn = CorrBlock(fmap1.float(), fmap2.float(), radius=self.hparams.corr_radius)
+
+        net, inp = torch.split(self.cnet(image0), [hdim, cdim], dim=1)
+        net = torch.tanh(net)
+        inp = torch.relu(inp)
+
+        coords0, coords1 = self.initialize_flow(image0)
+        if flow_init is not None:
+            coords1 = coords1 + flow_init
+
+        flow_predictions = []
+        flow_up = None
+        for itr in range(iters):
+            coords1 = coords1.detach()
+            corr = corr_fn(coords1)
+            flow = coords1 - coords0
+            net, up_mask, delta_flow = self.update_block(net, inp, corr, flow)
+            coords1 = coords1 + delta_flow
+            if test_mode and itr != iters - 1:
+                continue  # Q11: intermediate upsamplings are never returned in test mode
+            if up_mask is None:
+                flow_up = upflow8(coords1 - coords0)
+            else:
+                flow_up = self.upsample_flow(coords1 - coords0, up_mask)
+            flow_predictions.append(flow_up)
+
+        if test_mode:
+            return coords1 - coords0, flow_up
+        return flow_predictions

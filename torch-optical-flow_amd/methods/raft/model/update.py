@@ -1,0 +1,89 @@
+"""GRU update block (reference: methods/raft/model/update.py:40-161).
+
+Consumes the lookup output (B, L*(2r+1)^2, H, W) through ``encoder.convc1``. Convolutions run on
+PyTorch-ROCm (MIOpen); fusing the lookup into ``convc1`` is SURVEY §8(f) row 1 (next). Parameter names equal
+the reference's. ``ConvGRU`` (unused by RAFT) is not provided.
+"""
+from __future__ import annotations
+
+from typing import Tuple
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+from torch import Tensor
+
+
+class FlowHead(nn.Module):
+    def __init__(self, input_dim: int = 128, hidden_dim: int = 256) -> None:
+        super().__init__()
+        self.conv1 = nn.Conv2d(input_dim, hidden_dim, 3, padding=1)
+        self.conv2 = nn.Conv2d(hidden_dim, 2, 3, padding=1)
+        self.relu = nn.ReLU(inplace=True)
+
+    def forward(self, x: Tensor) -> Tensor:
+        return self.conv2(self.relu(self.conv1(x)))
+
+
+class SepConvGRU(nn.Module):
+    """GRU with a horizontal (1x5) then a vertical (5x1) pass (`update.py:69-107`)."""
+
+    def __init__(self, hidden_dim: int = 128, input_dim: int = 192 + 128) -> None:
+        super().__init__()
+        cin = hidden_dim + input_dim
+        self.convz1 = nn.Conv2d(cin, hidden_dim, (1, 5), padding=(0, 2))
+        self.convr1 = nn.Conv2d(cin, hidden_dim, (1, 5), padding=(0, 2))
+        self.convq1 = nn.Conv2d(cin, hidden_dim, (1, 5), padding=(0, 2))
+        self.convz2 = nn.Conv2d(cin, hidden_dim, (5, 1), padding=(2, 0))
+        self.convr2 = nn.Conv2d(cin, hidden_dim, (5, 1), padding=(2, 0))
+        self.convq2 = nn.Conv2d(cin, hidden_dim, (5, 1), padding=(2, 0))
+
+    @staticmethod
+    def _step(h: Tensor, x: Tensor, convz: nn.Module, convr: nn.Module, convq: nn.Module) -> Tensor:
+        hx = torch.cat([h, x], dim=1)
+        z = torch.sigmoid(convz(hx))
+        r = torch.sigmoid(convr(hx))
+        q = torch.tanh(convq(torch.cat([r * h, x], dim=1)))
+        return (1 - z) * h + z * q
+
+    def forward(self, h: Tensor, x: Tensor) -> Tensor:
+        h = self._step(h, x, self.convz1, self.convr1, self.convq1)
+        return self._step(h, x, self.convz2, self.convr2, self.convq2)
+
+
+class BasicMotionEncoder(nn.Module):
+    """Correlation (1x1 then 3x3) and flow (7x7 then 3x3) branches fused by a 3x3 conv (`update.py:110-128`)."""
+
+    def __init__(self, corr_levels: int, corr_radius: int) -> None:
+        super().__init__()
+        corr_planes = corr_levels * (2 * corr_radius + 1) ** 2
+        self.convc1 = nn.Conv2d(corr_planes, 256, 1, padding=0)
+        self.convc2 = nn.Conv2d(256, 192, 3, padding=1)
+        self.convf1 = nn.Conv2d(2, 128, 7, padding=3)
+        self.convf2 = nn.Conv2d(128, 64, 3, padding=1)
+        self.conv = nn.Conv2d(64 + 192, 128 - 2, 3, padding=1)
+
+    def forward(self, flow: Tensor, corr: Tensor) -> Tensor:
+        cor = F.relu(self.convc2(F.relu(self.convc1(corr))))
+        flo = F.relu(self.convf2(F.relu(self.convf1(flow))))
+        out = F.relu(self.conv(torch.cat([cor, flo], dim=1)))
+        return torch.cat([out, flow], dim=1)
+
+
+class BasicUpdateBlock(nn.Module):
+    """Motion encoder -> SepConvGRU -> flow head, plus the convex-upsampling mask head x0.25 (`update.py:131-161`)."""
+
+    def __init__(self, corr_levels: int, corr_radius: int, hidden_dim: int = 128) -> None:
+        super().__init__()
+        self.encoder = BasicMotionEncoder(corr_levels, corr_radius)
+        self.gru = SepConvGRU(hidden_dim=hidden_dim, input_dim=128 + hidden_dim)
+        self.flow_head = FlowHead(hidden_dim, hidden_dim=256)
+        self.mask = nn.Sequential(
+            nn.Conv2d(128, 256, 3, padding=1), nn.ReLU(inplace=True), nn.Conv2d(256, 64 * 9, 1, padding=0)
+        )
+
+    def forward(self, net: Tensor, inp: Tensor, corr: Tensor, flow: Tensor) -> Tuple[Tensor, Tensor, Tensor]:
+        motion = self.encoder(flow, corr)
+        net = self.gru(net, torch.cat([inp, motion], dim=1))
+        delta_flow = self.flow_head(net)
+        return net, 0.25 * self.mask(net), delta_flow

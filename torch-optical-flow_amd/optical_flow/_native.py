@@ -1,0 +1,270 @@
+"""ctypes binding of liboflow_hip.so (C ABI declared in include/oflow.h) for torch tensors.
+
+PyTorch supplies device memory (its caching allocator) and the current HIP stream; the arithmetic runs in the
+hand-written gfx950 kernels of ``csrc/``. There is no fallback: on a tensor that is not on a ROCm GPU, or when
+the library is missing, every entry point raises ``RuntimeError``.
+
+``torch`` is imported before the library is opened so that the library's ``libamdhip64.so.7`` dependency
+resolves (by SONAME) to the HIP runtime PyTorch already loaded: one runtime, one set of streams.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from typing import List, Sequence
+
+import torch
+
+_LIB_PATH = os.environ.get(
+    "OFLOW_LIB", os.path.join(os.path.dirname(os.path.abspath(__file__)), "_lib", "liboflow_hip.so")
+)
+ABI_VERSION = 1
+MAX_LEVELS = 8
+MAX_RADIUS = 7
+E_TINY = -4
+
+INTERP = {"bilinear": 0, "nearest": 1, "bicubic": 2}
+PADDING = {"zeros": 0, "border": 1, "reflection": 2}
+
+# every symbol include/oflow.h declares (tests check the library exports them all)
+SYMBOLS = (
+    "oflow_abi_version",
+    "oflow_status_string",
+    "oflow_corr_pyramid_dims",
+    "oflow_corr_pyramid_f32",
+    "oflow_corr_lookup_f32",
+    "oflow_grid_warp_f32",
+    "oflow_grid_sample_f32",
+)
+
+_lib = None
+_recorder = None  # optional {op name: [(start event, end event), ...]} filled around each launch
+
+
+def set_event_recorder(recorder):
+    """Record a HIP event pair on the launch stream around every kernel launch (bench instrumentation).
+    ``recorder`` is a dict (op name -> list of (start, end) ``torch.cuda.Event``) or None to stop."""
+    global _recorder
+    _recorder = recorder
+
+
+class _Timed:
+    __slots__ = ("what", "stream", "ev0")
+
+    def __init__(self, what: str, device: torch.device):
+        self.what = what
+        self.stream = torch.cuda.current_stream(device) if _recorder is not None else None
+        self.ev0 = None
+
+    def __enter__(self):
+        if self.stream is not None:
+            self.ev0 = torch.cuda.Event(enable_timing=True)
+            self.ev0.record(self.stream)
+        return self
+
+    def __exit__(self, *exc):
+        if self.stream is not None and exc[0] is None and _recorder is not None:
+            ev1 = torch.cuda.Event(enable_timing=True)
+            ev1.record(self.stream)
+            _recorder.setdefault(self.what, []).append((self.ev0, ev1))
+        return False
+
+
+def library_path() -> str:
+    return _LIB_PATH
+
+
+def load() -> ctypes.CDLL:
+    """Open liboflow_hip.so once and declare the C signatures. Raises RuntimeError if it cannot."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(_LIB_PATH):
+        raise RuntimeError(
+            f"liboflow_hip.so not found at {_LIB_PATH}: build it with `make -C torch-optical-flow_amd/csrc` "
+            "(or __graft_entry__.build()); the MI355X path has no CPU fallback"
+        )
+    lib = ctypes.CDLL(_LIB_PATH)
+    P, I, F = ctypes.c_void_p, ctypes.c_int, ctypes.c_float
+    IP = ctypes.POINTER(ctypes.c_int)
+    PP = ctypes.POINTER(ctypes.c_void_p)
+    lib.oflow_abi_version.restype = I
+    lib.oflow_abi_version.argtypes = []
+    lib.oflow_status_string.restype = ctypes.c_char_p
+    lib.oflow_status_string.argtypes = [I]
+    lib.oflow_corr_pyramid_dims.restype = I
+    lib.oflow_corr_pyramid_dims.argtypes = [I, I, I, IP, IP]
+    lib.oflow_corr_pyramid_f32.restype = I
+    lib.oflow_corr_pyramid_f32.argtypes = [P, P, I, I, I, I, I, PP, P]
+    lib.oflow_corr_lookup_f32.restype = I
+    lib.oflow_corr_lookup_f32.argtypes = [PP, IP, IP, I, P, I, I, I, I, P, P]
+    lib.oflow_grid_warp_f32.restype = I
+    lib.oflow_grid_warp_f32.argtypes = [P, P, I, I, I, I, I, I, I, P, P]
+    lib.oflow_grid_sample_f32.restype = I
+    lib.oflow_grid_sample_f32.argtypes = [P, P, I, I, I, I, I, I, I, I, I, P, P]
+    v = lib.oflow_abi_version()
+    if v != ABI_VERSION:
+        raise RuntimeError(f"liboflow_hip.so ABI version {v}, expected {ABI_VERSION}: rebuild the library")
+    _lib = lib
+    return lib
+
+
+def _check(status: int, what: str) -> None:
+    if status == 0:
+        return
+    msg = load().oflow_status_string(status).decode()
+    if status == E_TINY:
+        raise ValueError(f"{what}: {msg}")
+    raise RuntimeError(f"{what} failed ({status}): {msg}")
+
+
+def _gpu_f32(t: torch.Tensor, name: str, what: str) -> torch.Tensor:
+    if not isinstance(t, torch.Tensor):
+        raise TypeError(f"{what}: {name} must be a torch.Tensor")
+    if t.device.type != "cuda":
+        raise RuntimeError(
+            f"{what}: {name} is on {t.device}; this MI355X build runs only on ROCm GPU tensors (no CPU fallback)"
+        )
+    if t.dtype != torch.float32:
+        t = t.float()
+    return t.contiguous()
+
+
+def _stream(device: torch.device) -> ctypes.c_void_p:
+    return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
+
+
+def pyramid_dims(h: int, w: int, num_levels: int):
+    hs = (ctypes.c_int * MAX_LEVELS)()
+    ws = (ctypes.c_int * MAX_LEVELS)()
+    _check(load().oflow_corr_pyramid_dims(h, w, num_levels, hs, ws), "corr_pyramid_dims")
+    return [(hs[i], ws[i]) for i in range(num_levels)]
+
+
+def corr_pyramid(fmap1: torch.Tensor, fmap2: torch.Tensor, num_levels: int = 4) -> List[torch.Tensor]:
+    """Level l of the all-pairs correlation pyramid as (B*H*W, 1, H_l, W_l) fp32 views of one allocation."""
+    what = "corr_pyramid"
+    f1 = _gpu_f32(fmap1, "fmap1", what)
+    f2 = _gpu_f32(fmap2, "fmap2", what)
+    if f1.dim() != 4 or f1.shape != f2.shape:
+        raise RuntimeError(f"{what}: fmap1 {tuple(fmap1.shape)} and fmap2 {tuple(fmap2.shape)} must be equal (B, C, H, W)")
+    if f1.device != f2.device:
+        raise RuntimeError(f"{what}: fmap1 and fmap2 are on different devices")
+    b, c, h, w = f1.shape
+    dims = pyramid_dims(h, w, num_levels)
+    if b == 0:
+        return [torch.empty((0, 1, hl, wl), device=f1.device) for hl, wl in dims]
+    if any(hl < 1 or wl < 1 for hl, wl in dims):
+        raise RuntimeError(f"{what}: {num_levels} levels of 2x2 pooling need H, W >= {2 ** (num_levels - 1)}")
+    q = b * h * w
+    sizes = [q * hl * wl for hl, wl in dims]
+    buf = torch.empty(sum(sizes), device=f1.device, dtype=torch.float32)
+    levels, off = [], 0
+    for (hl, wl), n in zip(dims, sizes):
+        levels.append(buf[off : off + n].view(q, 1, hl, wl))
+        off += n
+    ptrs = (ctypes.c_void_p * num_levels)(*[lv.data_ptr() for lv in levels])
+    with torch.cuda.device(f1.device), _Timed("corr_pyramid", f1.device):
+        _check(
+            load().oflow_corr_pyramid_f32(
+                f1.data_ptr(), f2.data_ptr(), b, c, h, w, num_levels, ptrs, _stream(f1.device)
+            ),
+            what,
+        )
+    return levels
+
+
+def corr_lookup(levels: Sequence[torch.Tensor], coords: torch.Tensor, radius: int) -> torch.Tensor:
+    """(B, L*(2r+1)^2, H, W) fp32 windowed lookup of ``levels`` at ``coords`` (B, 2, H, W)."""
+    what = "corr_lookup"
+    co = _gpu_f32(coords, "coords", what)
+    if co.dim() != 4 or co.shape[1] != 2:
+        raise RuntimeError(f"{what}: coords must be (B, 2, H, W), got {tuple(coords.shape)}")
+    b, _, h, w = co.shape
+    nl = len(levels)
+    if not 1 <= nl <= MAX_LEVELS:
+        raise RuntimeError(f"{what}: number of pyramid levels {nl} outside [1, {MAX_LEVELS}]")
+    if not 0 <= int(radius) <= MAX_RADIUS:
+        raise RuntimeError(f"{what}: radius {radius} outside [0, {MAX_RADIUS}]")
+    lv = []
+    for i, t in enumerate(levels):
+        t = _gpu_f32(t, f"corr_pyramid[{i}]", what)
+        if t.device != co.device:
+            raise RuntimeError(f"{what}: corr_pyramid[{i}] and coords are on different devices")
+        if t.dim() != 4 or t.shape[0] != b * h * w or t.shape[1] != 1:
+            raise RuntimeError(f"{what}: corr_pyramid[{i}] shape {tuple(t.shape)} != ({b * h * w}, 1, H_l, W_l)")
+        lv.append(t)
+    k = 2 * int(radius) + 1
+    out = torch.empty((b, nl * k * k, h, w), device=co.device, dtype=torch.float32)
+    if out.numel() == 0:
+        return out
+    ptrs = (ctypes.c_void_p * nl)(*[t.data_ptr() for t in lv])
+    hs = (ctypes.c_int * nl)(*[int(t.shape[2]) for t in lv])
+    ws = (ctypes.c_int * nl)(*[int(t.shape[3]) for t in lv])
+    with torch.cuda.device(co.device), _Timed("corr_lookup", co.device):
+        _check(
+            load().oflow_corr_lookup_f32(
+                ptrs, hs, ws, nl, co.data_ptr(), b, h, w, int(radius), out.data_ptr(), _stream(co.device)
+            ),
+            what,
+        )
+    return out
+
+
+def _modes(mode: str, padding_mode: str, what: str):
+    if mode not in INTERP:
+        raise ValueError(f"{what}: nn.functional.grid_sample(): expected mode to be 'bilinear', 'nearest' or 'bicubic', but got: '{mode}'")
+    if padding_mode not in PADDING:
+        raise ValueError(
+            f"{what}: nn.functional.grid_sample(): expected padding_mode to be 'zeros', 'border', or 'reflection', but got: '{padding_mode}'"
+        )
+    return INTERP[mode], PADDING[padding_mode]
+
+
+def grid_warp(frame: torch.Tensor, flow: torch.Tensor, mode: str, padding_mode: str, align_corners: bool) -> torch.Tensor:
+    """grid_sample(frame, linspace-grid + flow) with the grid never materialised."""
+    what = "warp"
+    m, p = _modes(mode, padding_mode, what)
+    fr = _gpu_f32(frame, "frame", what)
+    fl = _gpu_f32(flow, "flow", what)
+    if fr.dim() != 4 or fl.dim() != 4 or fl.shape[1] != 2 or fl.shape[0] != fr.shape[0] or fl.shape[2:] != fr.shape[2:]:
+        raise RuntimeError(f"{what}: frame {tuple(frame.shape)} must be (B, C, H, W) and flow {tuple(flow.shape)} (B, 2, H, W)")
+    if fr.device != fl.device:
+        raise RuntimeError(f"{what}: frame and flow are on different devices")
+    b, c, h, w = fr.shape
+    out = torch.empty_like(fr)
+    if out.numel() == 0:
+        return out
+    with torch.cuda.device(fr.device), _Timed("grid_warp", fr.device):
+        _check(
+            load().oflow_grid_warp_f32(
+                fr.data_ptr(), fl.data_ptr(), b, c, h, w, m, p, int(bool(align_corners)), out.data_ptr(), _stream(fr.device)
+            ),
+            what,
+        )
+    return out
+
+
+def grid_sample(inp: torch.Tensor, grid: torch.Tensor, mode: str, padding_mode: str, align_corners: bool) -> torch.Tensor:
+    """F.grid_sample for 4-D input (B, C, H, W) and grid (B, Ho, Wo, 2)."""
+    what = "grid_sample"
+    m, p = _modes(mode, padding_mode, what)
+    x = _gpu_f32(inp, "input", what)
+    g = _gpu_f32(grid, "grid", what)
+    if x.dim() != 4 or g.dim() != 4 or g.shape[-1] != 2 or g.shape[0] != x.shape[0]:
+        raise RuntimeError(f"{what}: input {tuple(inp.shape)} must be (B, C, H, W) and grid {tuple(grid.shape)} (B, Ho, Wo, 2)")
+    if x.device != g.device:
+        raise RuntimeError(f"{what}: input and grid are on different devices")
+    b, c, h, w = x.shape
+    ho, wo = g.shape[1], g.shape[2]
+    out = torch.empty((b, c, ho, wo), device=x.device, dtype=torch.float32)
+    if out.numel() == 0:
+        return out
+    with torch.cuda.device(x.device):
+        _check(
+            load().oflow_grid_sample_f32(
+                x.data_ptr(), g.data_ptr(), b, c, h, w, ho, wo, m, p, int(bool(align_corners)), out.data_ptr(), _stream(x.device)
+            ),
+            what,
+        )
+    return out
