@@ -1,0 +1,77 @@
+"""Kernel micro-bench: corr_pyramid and corr_lookup alone at BASELINE shapes, HIP-event timed (median of N).
+
+    python tools/kbench.py [--shape sintel8|corr4|kitti8|hd1] [--iters 20]
+"""
+import argparse
+import json
+import os
+import statistics
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PKG = os.path.join(REPO, "torch-optical-flow_amd")
+for p in (REPO, PKG, os.path.join(PKG, "methods", "raft")):
+    sys.path.insert(0, p)
+
+import torch  # noqa: E402
+
+from bench import lookup_bytes, pyramid_cost  # noqa: E402
+from model import synthetic  # noqa: E402
+from model.utils import coords_grid  # noqa: E402
+from optical_flow import _native  # noqa: E402
+
+SHAPES = {"sintel8": (8, 55, 128), "corr4": (4, 128, 128), "kitti8": (8, 47, 156), "sintel1": (1, 55, 128), "hd1": (1, 135, 240)}
+
+
+def timed(fn, iters):
+    ts = []
+    for _ in range(iters):
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record()
+        fn()
+        b.record()
+        b.synchronize()
+        ts.append(a.elapsed_time(b))
+    return statistics.median(ts), min(ts)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--shape", default="sintel8", choices=sorted(SHAPES))
+    ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--sigma", type=float, default=4.0)
+    args = ap.parse_args()
+    b, h, w = SHAPES[args.shape]
+    dev = torch.device("cuda", 0)
+    f1, f2 = synthetic.synthetic_fmaps(b, 256, h, w, stream=3)
+    f1, f2 = f1.to(dev), f2.to(dev)
+    coords = (coords_grid(b, h, w) + torch.from_numpy(synthetic.hash_normal(4, (b, 2, h, w), args.sigma))).to(dev)
+    pyr = _native.corr_pyramid(f1, f2, 4)
+    torch.cuda.synchronize()
+    dims = [(int(p.shape[2]), int(p.shape[3])) for p in pyr]
+    del pyr
+    torch.cuda.empty_cache()
+    pm, pmin = timed(lambda: _native.corr_pyramid(f1, f2, 4), args.iters)
+    pyr = _native.corr_pyramid(f1, f2, 4)
+    lm, lmin = timed(lambda: _native.corr_lookup(pyr, coords, 4), args.iters * 5)
+    flops, pbytes = pyramid_cost(b, dims)
+    lb = lookup_bytes(b, dims)
+    print(
+        json.dumps(
+            {
+                "shape": args.shape,
+                "pyramid_ms": round(pm, 4),
+                "pyramid_tflops": round(flops / pm / 1e9, 2),
+                "pyramid_min_ms": round(pmin, 4),
+                "pyramid_GBs": round(pbytes / pm / 1e6, 1),
+                "lookup_ms": round(lm, 5),
+                "lookup_min_ms": round(lmin, 5),
+                "lookup_GBs": round(lb / lm / 1e6, 1),
+                "lookup_bytes": lb,
+            }
+        )
+    )
+
+
+if __name__ == "__main__":
+    main()
