@@ -93,6 +93,20 @@ int oflow_grid_warp_f32(const float* d_frame, const float* d_flow, int B, int C,
 int oflow_grid_sample_f32(const float* d_input, const float* d_grid, int B, int C, int H, int W, int Ho, int Wo,
                           int mode, int padding_mode, int align_corners, float* d_out, void* stream);
 
+/*
+ * On-the-fly fp16 correlation (memory-efficient path for large frames; BASELINE configs[4], no volume).
+ * Same output as oflow_corr_lookup_f32 on the dense pyramid of (fmap1, fmap2), by linearity of the pooling:
+ * level-l correlations are dot products of fmap1 with the floor 2^l-pooled fmap2 (corr.py:38-54, 79-87).
+ *   prepare: d_f1h = fmap1 / sqrt(C) as (B, H, W, C) fp16; d_f2h[l] = pool_l(fmap2) as (B, H_l, W_l, C) fp16,
+ *            pooled in fp32 (d_scratch: B*C*sum_{l>=1} H_l*W_l floats) then rounded. C % 32 == 0.
+ *   lookup:  d_out (B, L*(2r+1)^2, H, W) fp32, radius <= 4; window dot products on v_mfma_f32_16x16x32_f16.
+ */
+int oflow_corr_otf_prepare_f16(const float* d_fmap1, const float* d_fmap2, int B, int C, int H, int W,
+                               int num_levels, void* d_f1h, void* const* d_f2h, float* d_scratch, void* stream);
+int oflow_corr_lookup_otf_f16(const void* d_f1h, const void* const* d_f2h, const int* level_h, const int* level_w,
+                              int num_levels, const float* d_coords, int B, int C, int H, int W, int radius,
+                              float* d_out, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -23,16 +23,21 @@ from optical_flow import _native  # noqa: E402
 SHAPES = {"sintel8": (8, 55, 128), "corr4": (4, 128, 128), "kitti8": (8, 47, 156), "sintel1": (1, 55, 128), "hd1": (1, 135, 240)}
 
 
-def timed(fn, iters):
-    ts = []
-    for _ in range(iters):
+def timed(fn, n=50):
+    """Mean per-launch time of n back-to-back launches between one event pair (median of 3 rounds): the queue
+    stays ahead of the GPU, so host launch latency is not in the number."""
+    fn()
+    torch.cuda.synchronize()
+    rounds = []
+    for _ in range(3):
         a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         a.record()
-        fn()
+        for _ in range(n):
+            fn()
         b.record()
         b.synchronize()
-        ts.append(a.elapsed_time(b))
-    return statistics.median(ts), min(ts)
+        rounds.append(a.elapsed_time(b) / n)
+    return statistics.median(rounds)
 
 
 def main():
@@ -51,9 +56,9 @@ def main():
     dims = [(int(p.shape[2]), int(p.shape[3])) for p in pyr]
     del pyr
     torch.cuda.empty_cache()
-    pm, pmin = timed(lambda: _native.corr_pyramid(f1, f2, 4), args.iters)
+    pm = timed(lambda: _native.corr_pyramid(f1, f2, 4), args.iters)
     pyr = _native.corr_pyramid(f1, f2, 4)
-    lm, lmin = timed(lambda: _native.corr_lookup(pyr, coords, 4), args.iters * 5)
+    lm = timed(lambda: _native.corr_lookup(pyr, coords, 4), args.iters * 5)
     flops, pbytes = pyramid_cost(b, dims)
     lb = lookup_bytes(b, dims)
     print(
@@ -62,10 +67,8 @@ def main():
                 "shape": args.shape,
                 "pyramid_ms": round(pm, 4),
                 "pyramid_tflops": round(flops / pm / 1e9, 2),
-                "pyramid_min_ms": round(pmin, 4),
                 "pyramid_GBs": round(pbytes / pm / 1e6, 1),
                 "lookup_ms": round(lm, 5),
-                "lookup_min_ms": round(lmin, 5),
                 "lookup_GBs": round(lb / lm / 1e6, 1),
                 "lookup_bytes": lb,
             }

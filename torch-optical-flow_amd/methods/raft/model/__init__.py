@@ -12,8 +12,8 @@ try:
 except ImportError:  # pragma: no cover - path bootstrap
     _sys.path.insert(0, _os.path.abspath(_os.path.join(_os.path.dirname(__file__), "..", "..", "..")))
 
-from .corr import CorrBlock  # noqa: E402
+from .corr import AlternateCorrBlock, CorrBlock  # noqa: E402
 from .raft import RAFT  # noqa: E402
 from .utils import InputPadder, bilinear_sampler, coords_grid, upflow8  # noqa: E402
 
-__all__ = ["RAFT", "CorrBlock", "InputPadder", "bilinear_sampler", "coords_grid", "upflow8"]
+__all__ = ["RAFT", "AlternateCorrBlock", "CorrBlock", "InputPadder", "bilinear_sampler", "coords_grid", "upflow8"]

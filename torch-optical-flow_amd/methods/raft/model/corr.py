@@ -32,3 +32,21 @@ class CorrBlock:
         """All-pairs volume (B, H, W, 1, H, W) / sqrt(C) (`corr.py:79-87`)."""
         b, _, h, w = fmap1.shape
         return _native.corr_pyramid(fmap1, fmap2, 1)[0].view(b, h, w, 1, h, w)
+
+
+class AlternateCorrBlock:
+    """Memory-efficient correlation lookup (no (HW)^2 volume): same interface and output as ``CorrBlock``.
+
+    Level-l correlations are computed on demand as dot products of fmap1 with the floor 2^l-pooled fmap2, which
+    equals the dense pyramid by linearity of the pooling (`corr.py:38-54, 79-87`). Features are stored as NHWC
+    fp16 and multiplied on v_mfma_f32_16x16x32_f16 with fp32 accumulation (BASELINE configs[4]: 1080p, fp16);
+    outputs are fp32 like ``CorrBlock`` (Q5). Holds O(B*C*H*W) memory instead of O(B*(H*W)^2).
+    """
+
+    def __init__(self, fmap1: Tensor, fmap2: Tensor, num_levels: int = 4, radius: int = 4) -> None:
+        self.num_levels = num_levels
+        self.radius = radius
+        self.fmap1_f16, self.fmap2_pyramid_f16 = _native.otf_prepare(fmap1, fmap2, num_levels)
+
+    def __call__(self, coords: Tensor) -> Tensor:
+        return _native.corr_lookup_otf(self.fmap1_f16, self.fmap2_pyramid_f16, coords, self.radius)

@@ -5,6 +5,8 @@ LightningModule, so its checkpoints load unchanged; the training loop (`raft.py:
 W&B logging) is out of scope. ``forward`` keeps the reference's semantics and return
 values; three output-identical changes remove host work from the loop:
   * the correlation pyramid and every lookup run on the gfx950 kernels (``model.corr.CorrBlock``);
+    ``alternate_corr=True`` (an addition, default off) swaps in the volume-free fp16 ``AlternateCorrBlock``
+    for large frames;
   * coordinate grids are built on the device (no CPU build + H2D copy, `raft.py:68-69`);
   * with ``test_mode=True`` only the last iteration's convex upsampling is computed — the reference computes
     all ``iters`` and returns only the last (Q11, `raft.py:136-145`).
@@ -19,7 +21,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 from torch import Tensor
 
-from .corr import CorrBlock
+from .corr import AlternateCorrBlock, CorrBlock
 from .extractor import BasicEncoder
 from .update import BasicUpdateBlock
 from .utils import coords_grid, upflow8
@@ -54,6 +56,7 @@ class RAFT(nn.Module):
         lr: float = 0.00002,
         wdecay: float = 0.00005,
         epsilon: float = 1e-8,
+        alternate_corr: bool = False,
     ) -> None:
         super().__init__()
         self.hparams = HParams(
@@ -68,6 +71,7 @@ class RAFT(nn.Module):
             lr=lr,
             wdecay=wdecay,
             epsilon=epsilon,
+            alternate_corr=alternate_corr,
         )
         self.fnet = BasicEncoder(output_dim=256, norm_fn="instance", dropout=dropout)
         self.cnet = BasicEncoder(output_dim=hidden_dim + context_dim, norm_fn="batch", dropout=dropout)
@@ -130,7 +134,8 @@ class RAFT(nn.Module):
         hdim, cdim = self.hparams.hidden_dim, self.hparams.context_dim
 
         fmap1, fmap2 = self.fnet([image0, image1])
-        corr_fn = CorrBlock(fmap1.float(), fmap2.float(), radius=self.hparams.corr_radius)
+        block = AlternateCorrBlock if self.hparams.get("alternate_corr", False) else CorrBlock
+        corr_fn = block(fmap1.float(), fmap2.float(), radius=self.hparams.corr_radius)
 
         net, inp = torch.split(self.cnet(image0), [hdim, cdim], dim=1)
         net = torch.tanh(net)

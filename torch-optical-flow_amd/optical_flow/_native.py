@@ -35,6 +35,8 @@ SYMBOLS = (
     "oflow_corr_lookup_f32",
     "oflow_grid_warp_f32",
     "oflow_grid_sample_f32",
+    "oflow_corr_otf_prepare_f16",
+    "oflow_corr_lookup_otf_f16",
 )
 
 _lib = None
@@ -102,6 +104,10 @@ def load() -> ctypes.CDLL:
     lib.oflow_grid_warp_f32.argtypes = [P, P, I, I, I, I, I, I, I, P, P]
     lib.oflow_grid_sample_f32.restype = I
     lib.oflow_grid_sample_f32.argtypes = [P, P, I, I, I, I, I, I, I, I, I, P, P]
+    lib.oflow_corr_otf_prepare_f16.restype = I
+    lib.oflow_corr_otf_prepare_f16.argtypes = [P, P, I, I, I, I, I, P, PP, P, P]
+    lib.oflow_corr_lookup_otf_f16.restype = I
+    lib.oflow_corr_lookup_otf_f16.argtypes = [P, PP, IP, IP, I, P, I, I, I, I, I, P, P]
     v = lib.oflow_abi_version()
     if v != ABI_VERSION:
         raise RuntimeError(f"liboflow_hip.so ABI version {v}, expected {ABI_VERSION}: rebuild the library")
@@ -264,6 +270,73 @@ def grid_sample(inp: torch.Tensor, grid: torch.Tensor, mode: str, padding_mode: 
         _check(
             load().oflow_grid_sample_f32(
                 x.data_ptr(), g.data_ptr(), b, c, h, w, ho, wo, m, p, int(bool(align_corners)), out.data_ptr(), _stream(x.device)
+            ),
+            what,
+        )
+    return out
+
+
+def otf_prepare(fmap1: torch.Tensor, fmap2: torch.Tensor, num_levels: int = 4):
+    """fmap1/sqrt(C) and the floor-pooled fmap2 pyramid as NHWC fp16 tensors (on-the-fly correlation inputs).
+    Returns (f1h (B, H, W, C), [f2h_l (B, H_l, W_l, C)])."""
+    what = "corr_otf_prepare"
+    f1 = _gpu_f32(fmap1, "fmap1", what)
+    f2 = _gpu_f32(fmap2, "fmap2", what)
+    if f1.dim() != 4 or f1.shape != f2.shape or f1.device != f2.device:
+        raise RuntimeError(f"{what}: fmap1 {tuple(fmap1.shape)} and fmap2 {tuple(fmap2.shape)} must be equal (B, C, H, W) on one device")
+    b, c, h, w = f1.shape
+    if c % 32 != 0:
+        raise RuntimeError(f"{what}: the fp16 MFMA path needs C % 32 == 0, got C={c}")
+    dims = pyramid_dims(h, w, num_levels)
+    if any(hl < 1 or wl < 1 for hl, wl in dims):
+        raise RuntimeError(f"{what}: {num_levels} levels of 2x2 pooling need H, W >= {2 ** (num_levels - 1)}")
+    f1h = torch.empty((b, h, w, c), device=f1.device, dtype=torch.float16)
+    f2h = [torch.empty((b, hl, wl, c), device=f1.device, dtype=torch.float16) for hl, wl in dims]
+    if b == 0:
+        return f1h, f2h
+    scratch = torch.empty(max(1, b * c * sum(hl * wl for hl, wl in dims[1:])), device=f1.device, dtype=torch.float32)
+    ptrs = (ctypes.c_void_p * num_levels)(*[t.data_ptr() for t in f2h])
+    with torch.cuda.device(f1.device), _Timed("corr_otf_prepare", f1.device):
+        _check(
+            load().oflow_corr_otf_prepare_f16(
+                f1.data_ptr(), f2.data_ptr(), b, c, h, w, num_levels, f1h.data_ptr(), ptrs, scratch.data_ptr(), _stream(f1.device)
+            ),
+            what,
+        )
+    return f1h, f2h
+
+
+def corr_lookup_otf(f1h: torch.Tensor, f2h: Sequence[torch.Tensor], coords: torch.Tensor, radius: int) -> torch.Tensor:
+    """(B, L*(2r+1)^2, H, W) fp32 lookup computed from the fp16 feature pyramid, no correlation volume."""
+    what = "corr_lookup_otf"
+    co = _gpu_f32(coords, "coords", what)
+    if co.dim() != 4 or co.shape[1] != 2:
+        raise RuntimeError(f"{what}: coords must be (B, 2, H, W), got {tuple(coords.shape)}")
+    b, _, h, w = co.shape
+    if f1h.dtype != torch.float16 or tuple(f1h.shape[:3]) != (b, h, w) or not f1h.is_contiguous():
+        raise RuntimeError(f"{what}: f1h {tuple(f1h.shape)} must be contiguous fp16 ({b}, {h}, {w}, C)")
+    c = int(f1h.shape[3])
+    nl = len(f2h)
+    if not 1 <= nl <= MAX_LEVELS:
+        raise RuntimeError(f"{what}: number of pyramid levels {nl} outside [1, {MAX_LEVELS}]")
+    if not 0 <= int(radius) <= 4:
+        raise RuntimeError(f"{what}: radius {radius} outside [0, 4]")
+    for i, t in enumerate(f2h):
+        if t.dtype != torch.float16 or t.dim() != 4 or t.shape[0] != b or t.shape[3] != c or not t.is_contiguous():
+            raise RuntimeError(f"{what}: fmap2 level {i} {tuple(t.shape)} must be contiguous fp16 ({b}, H_l, W_l, {c})")
+        if t.device != co.device:
+            raise RuntimeError(f"{what}: fmap2 level {i} and coords are on different devices")
+    k = 2 * int(radius) + 1
+    out = torch.empty((b, nl * k * k, h, w), device=co.device, dtype=torch.float32)
+    if out.numel() == 0:
+        return out
+    ptrs = (ctypes.c_void_p * nl)(*[t.data_ptr() for t in f2h])
+    hs = (ctypes.c_int * nl)(*[int(t.shape[1]) for t in f2h])
+    ws = (ctypes.c_int * nl)(*[int(t.shape[2]) for t in f2h])
+    with torch.cuda.device(co.device), _Timed("corr_lookup_otf", co.device):
+        _check(
+            load().oflow_corr_lookup_otf_f16(
+                f1h.data_ptr(), ptrs, hs, ws, nl, co.data_ptr(), b, c, h, w, int(radius), out.data_ptr(), _stream(co.device)
             ),
             what,
         )
