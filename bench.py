@@ -38,9 +38,11 @@ MFMA_F32_PEAK_TFLOPS = 157.3  # dense fp32 MFMA (v_mfma_f32_32x32x2_f32), spec
 PMC_TRAFFIC_FILE = os.path.join(REPO, "profiles", "lookup_traffic.json")
 
 WORKLOADS = {
-    # name: (pairs per GPU, H, W, iters, padder mode)
-    "sintel": (8, 436, 1024, 12, "sintel"),
-    "kitti": (8, 375, 1242, 12, "sintel"),
+    # name: (pairs per GPU, H, W, iters, padder mode, alternate_corr)           BASELINE.json configs[...]
+    "sintel": (8, 436, 1024, 12, "sintel", False),  # [3] per rank (8 x 8 GPUs = 64); metric config
+    "kitti": (8, 375, 1242, 12, "sintel", False),  # [2] KITTI 1242x375, batch 8, fp32
+    "hd": (1, 1080, 1920, 12, "sintel", True),  # [4] 1080p, on-the-fly fp16 correlation
+    "corr": (4, 1024, 1024, 12, None, False),  # [1] corr build + 12 lookups only, 128x128x256 fmaps, batch 4
 }
 
 
@@ -124,24 +126,39 @@ def main() -> int:
     from model.pair_sharding import infer_sharded
     from optical_flow import _native
 
-    ppg, h, w, iters, pmode = WORKLOADS[args.workload]
+    ppg, h, w, iters, pmode, alt = WORKLOADS[args.workload]
     ppg = args.pairs_per_gpu or ppg
     global_batch = ppg * world
 
     torch.backends.cudnn.benchmark = bool(args.conv_benchmark)
-    model = RAFT().eval()
+    model = RAFT(alternate_corr=alt).eval()
     model.load_state_dict(synthetic.synthetic_state_dict(model.state_dict()))
     model = model.to(dev)
     if args.channels_last:
         model = model.to(memory_format=torch.channels_last)
 
     img0 = img1 = None
-    if rank == 0:  # two distinct pairs tiled to the global batch, resident in rank 0's HBM
+    if args.workload == "corr":  # configs[1]: fmaps (B, 256, 128, 128) ~ N(0, 1.45^2), coords = grid + N(0, 4^2)
+        from model import CorrBlock
+        from model.utils import coords_grid
+
+        f1, f2 = synthetic.synthetic_fmaps(ppg, 256, 128, 128, stream=0)
+        f1, f2 = f1.to(dev), f2.to(dev)
+        cgrid = (coords_grid(ppg, 128, 128) + torch.from_numpy(synthetic.hash_normal(1, (ppg, 2, 128, 128), 4.0))).to(dev)
+
+        def corr_step():
+            cb = CorrBlock(f1, f2)
+            out = None
+            for _ in range(iters):
+                out = cb(cgrid)
+            return out, out
+
+    elif rank == 0:  # two distinct pairs tiled to the global batch, resident in rank 0's HBM
         a0, a1 = synthetic.synthetic_pair(2, h, w, seed=0)
         reps = -(-global_batch // 2)
         img0 = a0.to(dev).repeat(reps, 1, 1, 1)[:global_batch].contiguous()
         img1 = a1.to(dev).repeat(reps, 1, 1, 1)[:global_batch].contiguous()
-    padder = InputPadder((h, w), mode=pmode)
+    padder = InputPadder((h, w), mode=pmode or "sintel")
 
     def forward(s0, s1):
         p0, p1 = padder.pad(s0, s1)
@@ -152,6 +169,8 @@ def main() -> int:
         return low, padder.unpad(up)
 
     def step():
+        if args.workload == "corr":
+            return corr_step()
         if world > 1:
             return infer_sharded(forward, img0, img1, dev)
         return forward(img0, img1)
@@ -179,7 +198,7 @@ def main() -> int:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
-    if rank == 0:
+    if rank == 0 and args.workload != "corr":
         assert out[1] is not None and out[1].shape == (global_batch, 2, h, w)
         assert torch.isfinite(out[1]).all()
     dims = _native.pyramid_dims((h + 7) // 8, (w + 7) // 8, 4)
@@ -195,10 +214,11 @@ def main() -> int:
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": "f32",
+        "dtype": "f16 features / f32 accumulate (corr); f32 elsewhere" if alt else "f32",
         "data": "synthetic (integer texture frames with a known (3, -1.5) px shift; hash-initialised weights)",
         "config": {
-            "workload": f"raft-{iters}iter-{args.workload}-{h}x{w}",
+            "workload": (f"corr-build+{iters}-lookups-fmaps-{ppg}x256x128x128" if args.workload == "corr"
+                         else f"raft-{iters}iter-{args.workload}-{h}x{w}" + ("-otf-fp16" if alt else "")),
             "pairs_per_gpu": ppg,
             "global_batch": global_batch,
             "iters": iters,
@@ -208,7 +228,14 @@ def main() -> int:
             "channels_last": bool(args.channels_last),
         },
     }
-    if rec:
+    if rec and alt:
+        lk = rec.get("corr_lookup_otf", [])
+        pp = rec.get("corr_otf_prepare", [])
+        line["kernels"] = {
+            "corr_lookup_otf": {"launch_ms": round(mean_ms(lk), 4), "launches": len(lk)},
+            "corr_otf_prepare": {"launch_ms": round(mean_ms(pp), 4) if pp else None},
+        }
+    elif rec:
         lk = rec.get("corr_lookup", [])
         pk = rec.get("corr_pyramid", [])
         lk_ms = mean_ms(lk)
@@ -247,7 +274,7 @@ def main() -> int:
                     "bytes_per_launch": nbytes,
                 }
             }
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and args.workload in ("sintel", "kitti"):
         line["cpu_baseline"] = cpu_baseline(h, w, iters)
     if rank == 0:
         print(json.dumps(line), flush=True)

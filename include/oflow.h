@@ -107,6 +107,22 @@ int oflow_corr_lookup_otf_f16(const void* d_f1h, const void* const* d_f2h, const
                               int num_levels, const float* d_coords, int B, int C, int H, int W, int radius,
                               float* d_out, void* stream);
 
+/*
+ * Fused elementwise stages of the update block around its (bias-free) MIOpen convolutions
+ * (methods/raft/model/update.py:69-161). Tensors are (B, C, P) with contiguous (C, P)
+ * parts and an explicit batch stride in floats, so they can be channel slices of concatenated buffers.
+ *   bias_act : y0[b,c,p] (and y1 if not NULL) = act(x[b,c,p] + bias[c]) * scale; act 0 none, 1 relu,
+ *              2 sigmoid, 3 tanh; bias may be NULL; y0 may alias x.
+ *   gru_reset: rh = sigmoid(zr[:, CH + c] + br[c]) * h          (zr = [z | r] pre-bias gate convolution)
+ *   gru_blend: h = (1 - z) * h + z * tanh(q + bq[c]), z = sigmoid(zr[:, c] + bz[c]); h updated in place
+ */
+int oflow_bias_act_f32(const float* d_x, long long sx, const float* d_bias, float* d_y0, long long sy0, float* d_y1,
+                       long long sy1, int B, int C, int P, int activation, float scale, void* stream);
+int oflow_gru_reset_f32(const float* d_zr, long long szr, const float* d_br, const float* d_h, long long sh,
+                        float* d_rh, long long srh, int B, int CH, int P, void* stream);
+int oflow_gru_blend_f32(const float* d_zr, long long szr, const float* d_bz, const float* d_q, long long sq,
+                        const float* d_bq, float* d_h, long long sh, int B, int CH, int P, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -68,3 +68,26 @@ def test_train_mode_returns_all_predictions():
         _, up = model(img0.to(DEV), img1.to(DEV), iters=3, test_mode=True)
     assert isinstance(preds, list) and len(preds) == 3
     assert torch.equal(preds[-1], up)
+
+
+def test_fused_update_matches_module_update_block():
+    """FusedUpdate (fused bias/activation/GRU kernels, merged z|r convolution, persistent [h | x] buffers) against
+    the nn.Module update block on the same GPU, two steps so the carried state is checked too."""
+    from model.update import FusedUpdate
+
+    model = _model(RAFT)
+    block = model.update_block
+    b, h, w = 2, 24, 40
+    g = lambda s, shape, std: torch.from_numpy(synthetic.hash_normal(s, shape, std)).to(DEV)
+    net, inp = torch.tanh(g(1, (b, 128, h, w), 1.0)), torch.relu(g(2, (b, 128, h, w), 1.0))
+    corr1, corr2 = g(3, (b, 324, h, w), 2.0), g(4, (b, 324, h, w), 2.0)
+    flow1, flow2 = g(5, (b, 2, h, w), 3.0), g(6, (b, 2, h, w), 3.0)
+    with torch.inference_mode():
+        n1, m1, d1 = block(net, inp, corr1, flow1)
+        n2, m2, d2 = block(n1, inp, corr2, flow2)
+        runner = FusedUpdate(block, net, inp)
+        f1 = runner.step(corr1, flow1)
+        f2 = runner.step(corr2, flow2)
+    for ref, got in zip((n1, m1, d1, n2, m2, d2), (*f1, *f2)):
+        err = float((ref - got).abs().max())
+        assert err <= 1e-4 * max(1.0, float(ref.abs().max())), err

@@ -59,6 +59,13 @@ def main():
     pm = timed(lambda: _native.corr_pyramid(f1, f2, 4), args.iters)
     pyr = _native.corr_pyramid(f1, f2, 4)
     lm = timed(lambda: _native.corr_lookup(pyr, coords, 4), args.iters * 5)
+    # warp operator at the SURVEY §8(d) shape: frame (8, 3, 436, 1024), flow = normalize(N(0, 8^2) px)
+    import optical_flow
+    frame, _ = synthetic.synthetic_pair(8, 436, 1024, seed=1)
+    flow = optical_flow.normalize(torch.from_numpy(synthetic.hash_normal(5, (8, 2, 436, 1024), 8.0)))
+    frame, flow = frame.to(dev), flow.to(dev)
+    wm = timed(lambda: optical_flow.warp(frame, flow), args.iters * 5)
+    wbytes = (2 * 3 + 2) * 4 * 8 * 436 * 1024
     flops, pbytes = pyramid_cost(b, dims)
     lb = lookup_bytes(b, dims)
     print(
@@ -71,6 +78,8 @@ def main():
                 "lookup_ms": round(lm, 5),
                 "lookup_GBs": round(lb / lm / 1e6, 1),
                 "lookup_bytes": lb,
+                "warp_ms": round(wm, 5),
+                "warp_GBs": round(wbytes / wm / 1e6, 1),
             }
         )
     )

@@ -9,7 +9,9 @@ values; three output-identical changes remove host work from the loop:
     for large frames;
   * coordinate grids are built on the device (no CPU build + H2D copy, `raft.py:68-69`);
   * with ``test_mode=True`` only the last iteration's convex upsampling is computed — the reference computes
-    all ``iters`` and returns only the last (Q11, `raft.py:136-145`).
+    all ``iters`` and returns only the last (Q11, `raft.py:136-145`);
+  * without autograd on the GPU the update block runs through ``FusedUpdate`` (fused bias/activation/GRU
+    elementwise kernels over persistent concatenated buffers; same weights and arithmetic up to rounding).
 """
 from __future__ import annotations
 
@@ -23,7 +25,7 @@ from torch import Tensor
 
 from .corr import AlternateCorrBlock, CorrBlock
 from .extractor import BasicEncoder
-from .update import BasicUpdateBlock
+from .update import BasicUpdateBlock, FusedUpdate
 from .utils import coords_grid, upflow8
 
 
@@ -76,6 +78,7 @@ class RAFT(nn.Module):
         self.fnet = BasicEncoder(output_dim=256, norm_fn="instance", dropout=dropout)
         self.cnet = BasicEncoder(output_dim=hidden_dim + context_dim, norm_fn="batch", dropout=dropout)
         self.update_block = BasicUpdateBlock(corr_levels=corr_levels, corr_radius=corr_radius, hidden_dim=hidden_dim)
+        self.fused_update = True  # plain attribute (not an hparam): False runs the nn.Module update block
 
     # -- checkpoints -------------------------------------------------------------------------------------
     @classmethod
@@ -145,13 +148,20 @@ class RAFT(nn.Module):
         if flow_init is not None:
             coords1 = coords1 + flow_init
 
+        # inference on the GPU: fused update block (same weights and math, persistent [h | x] buffers)
+        fused = net.is_cuda and not torch.is_grad_enabled() and self.fused_update
+        runner = FusedUpdate(self.update_block, net, inp) if fused else None
+
         flow_predictions = []
         flow_up = None
         for itr in range(iters):
             coords1 = coords1.detach()
             corr = corr_fn(coords1)
             flow = coords1 - coords0
-            net, up_mask, delta_flow = self.update_block(net, inp, corr, flow)
+            if runner is not None:
+                net, up_mask, delta_flow = runner.step(corr, flow)
+            else:
+                net, up_mask, delta_flow = self.update_block(net, inp, corr, flow)
             coords1 = coords1 + delta_flow
             if test_mode and itr != iters - 1:
                 continue  # Q11: intermediate upsamplings are never returned in test mode

@@ -13,6 +13,8 @@ import torch.nn as nn
 import torch.nn.functional as F
 from torch import Tensor
 
+from optical_flow import _native
+
 
 class FlowHead(nn.Module):
     def __init__(self, input_dim: int = 128, hidden_dim: int = 256) -> None:
@@ -87,3 +89,65 @@ class BasicUpdateBlock(nn.Module):
         net = self.gru(net, torch.cat([inp, motion], dim=1))
         delta_flow = self.flow_head(net)
         return net, 0.25 * self.mask(net), delta_flow
+
+
+class FusedUpdate:
+    """Inference-time execution of ``BasicUpdateBlock`` (same weights, same math) with fused elementwise work.
+
+    The GRU state and its input live in two persistent channel-concatenated buffers, ``hx = [h | inp | motion]``
+    and ``rhx = [r*h | inp | motion]``, so the four ``torch.cat`` copies per iteration (update.py:93, 96, 100,
+    103) and the ``[inp, motion]`` / ``[out, flow]`` cats (update.py:127, 155) disappear: the motion encoder's
+    last ReLU writes into both buffers and ``inp`` is written once per forward. Convolutions run on MIOpen without
+    bias; bias + activation run as one HIP pass (``oflow_bias_act_f32``). The z and r convolutions of each GRU half
+    are one convolution over concatenated weights (the gates are independent output channels), followed by
+    ``oflow_gru_reset_f32`` (r*h into ``rhx``) and, after the q convolution, ``oflow_gru_blend_f32`` (h updated
+    in place in ``hx``). Requires ROCm tensors and no autograd (it updates its state in place).
+    """
+
+    def __init__(self, block: BasicUpdateBlock, net: Tensor, inp: Tensor) -> None:
+        b, ch, h, w = net.shape
+        self.block, self.ch, self.ci = block, ch, inp.shape[1]
+        enc, gru = block.encoder, block.gru
+        cm = enc.conv.out_channels + 2
+        total = ch + self.ci + cm
+        if gru.convz1.in_channels != total:
+            raise RuntimeError("FusedUpdate: unexpected GRU input width")
+        self.hx = torch.empty((b, total, h, w), device=net.device, dtype=torch.float32)
+        self.rhx = torch.empty_like(self.hx)
+        self.hx[:, :ch].copy_(net)
+        self.hx[:, ch : ch + self.ci].copy_(inp)
+        self.rhx[:, ch : ch + self.ci].copy_(inp)
+        self.m0 = ch + self.ci  # first motion channel
+        self.halves = []
+        for tag, pad in (("1", (0, 2)), ("2", (2, 0))):
+            cz, cr, cq = (getattr(gru, f"conv{g}{tag}") for g in "zrq")
+            wzr = torch.cat([cz.weight, cr.weight], dim=0).contiguous()
+            self.halves.append((wzr, cz.bias.contiguous(), cr.bias.contiguous(), cq.weight, cq.bias.contiguous(), pad))
+
+    @staticmethod
+    def _conv(x: Tensor, conv: nn.Conv2d) -> Tensor:
+        return F.conv2d(x, conv.weight, None, conv.stride, conv.padding, conv.dilation, conv.groups)
+
+    def step(self, corr: Tensor, flow: Tensor) -> Tuple[Tensor, Tensor, Tensor]:
+        enc, blk = self.block.encoder, self.block
+        cor = _native.bias_act_(self._conv(corr, enc.convc1), enc.convc1.bias, "relu")
+        cor = _native.bias_act_(self._conv(cor, enc.convc2), enc.convc2.bias, "relu")
+        flo = _native.bias_act_(self._conv(flow, enc.convf1), enc.convf1.bias, "relu")
+        flo = _native.bias_act_(self._conv(flo, enc.convf2), enc.convf2.bias, "relu")
+        out = self._conv(torch.cat([cor, flo], dim=1), enc.conv)
+        m0, m1 = self.m0, self.m0 + out.shape[1]
+        _native.bias_act_(out, enc.conv.bias, "relu", out=self.hx[:, m0:m1], out2=self.rhx[:, m0:m1])
+        self.hx[:, m1:].copy_(flow)
+        self.rhx[:, m1:].copy_(flow)
+        h = self.hx[:, : self.ch]
+        for wzr, bz, br, wq, bq, pad in self.halves:
+            zr = F.conv2d(self.hx, wzr, None, 1, pad)
+            _native.gru_reset(zr, br, h, self.rhx[:, : self.ch])
+            q = F.conv2d(self.rhx, wq, None, 1, pad)
+            _native.gru_blend_(zr, bz, q, bq, h)
+        net = h.contiguous()
+        fh = blk.flow_head
+        delta_flow = fh.conv2(_native.bias_act_(self._conv(net, fh.conv1), fh.conv1.bias, "relu"))
+        m = _native.bias_act_(self._conv(net, blk.mask[0]), blk.mask[0].bias, "relu")
+        mask = _native.bias_act_(self._conv(m, blk.mask[2]), blk.mask[2].bias, "none", scale=0.25)
+        return net, mask, delta_flow

@@ -37,6 +37,9 @@ SYMBOLS = (
     "oflow_grid_sample_f32",
     "oflow_corr_otf_prepare_f16",
     "oflow_corr_lookup_otf_f16",
+    "oflow_bias_act_f32",
+    "oflow_gru_reset_f32",
+    "oflow_gru_blend_f32",
 )
 
 _lib = None
@@ -106,6 +109,13 @@ def load() -> ctypes.CDLL:
     lib.oflow_grid_sample_f32.argtypes = [P, P, I, I, I, I, I, I, I, I, I, P, P]
     lib.oflow_corr_otf_prepare_f16.restype = I
     lib.oflow_corr_otf_prepare_f16.argtypes = [P, P, I, I, I, I, I, P, PP, P, P]
+    L = ctypes.c_longlong
+    lib.oflow_bias_act_f32.restype = I
+    lib.oflow_bias_act_f32.argtypes = [P, L, P, P, L, P, L, I, I, I, I, F, P]
+    lib.oflow_gru_reset_f32.restype = I
+    lib.oflow_gru_reset_f32.argtypes = [P, L, P, P, L, P, L, I, I, I, P]
+    lib.oflow_gru_blend_f32.restype = I
+    lib.oflow_gru_blend_f32.argtypes = [P, L, P, P, L, P, P, L, I, I, I, P]
     lib.oflow_corr_lookup_otf_f16.restype = I
     lib.oflow_corr_lookup_otf_f16.argtypes = [P, PP, IP, IP, I, P, I, I, I, I, I, P, P]
     v = lib.oflow_abi_version()
@@ -341,3 +351,66 @@ def corr_lookup_otf(f1h: torch.Tensor, f2h: Sequence[torch.Tensor], coords: torc
             what,
         )
     return out
+
+
+ACT = {"none": 0, "relu": 1, "sigmoid": 2, "tanh": 3}
+
+
+def _chan_view(t: torch.Tensor, what: str):
+    """(B, C, H, W) fp32 CUDA tensor whose (C, H, W) part is contiguous -> (ptr, batch stride, C, P)."""
+    if t.device.type != "cuda" or t.dtype != torch.float32 or t.dim() != 4:
+        raise RuntimeError(f"{what}: expected a 4-D fp32 ROCm tensor, got {t.dtype} {tuple(t.shape)} on {t.device}")
+    b, c, h, w = t.shape
+    if t.stride(3) != 1 or t.stride(2) != w or t.stride(1) != h * w:
+        raise RuntimeError(f"{what}: the (C, H, W) part must be contiguous")
+    return t.data_ptr(), t.stride(0), c, h * w
+
+
+def bias_act_(x: torch.Tensor, bias, act: str = "relu", scale: float = 1.0, out=None, out2=None) -> torch.Tensor:
+    """out = act(x + bias[c]) * scale (in place when out is None); optionally also into out2."""
+    px, sx, c, p = _chan_view(x, "bias_act")
+    y = x if out is None else out
+    py, sy, cy, py_ = _chan_view(y, "bias_act out")
+    p2, s2 = (0, 0)
+    if out2 is not None:
+        p2, s2, c2, _ = _chan_view(out2, "bias_act out2")
+        if c2 != c:
+            raise RuntimeError("bias_act: out2 channel count differs")
+    if cy != c or py_ != p or y.shape[0] != x.shape[0]:
+        raise RuntimeError("bias_act: output shape differs from input")
+    if bias is not None and (bias.numel() != c or bias.dtype != torch.float32 or not bias.is_contiguous()):
+        raise RuntimeError("bias_act: bias must be a contiguous fp32 vector of C elements")
+    with torch.cuda.device(x.device):
+        _check(
+            load().oflow_bias_act_f32(
+                px, sx, bias.data_ptr() if bias is not None else None, py, sy, p2 or None, s2, x.shape[0], c, p,
+                ACT[act], float(scale), _stream(x.device)
+            ),
+            "bias_act",
+        )
+    return y
+
+
+def gru_reset(zr: torch.Tensor, br: torch.Tensor, h: torch.Tensor, rh: torch.Tensor) -> None:
+    """rh = sigmoid(zr[:, CH:] + br) * h  (zr = [z | r] pre-bias, CH = h channels)."""
+    pz, sz, c2, p = _chan_view(zr, "gru_reset zr")
+    ph, sh, ch, p1 = _chan_view(h, "gru_reset h")
+    pr, sr, cr, p2 = _chan_view(rh, "gru_reset rh")
+    if c2 != 2 * ch or cr != ch or p1 != p or p2 != p or br.numel() != ch:
+        raise RuntimeError("gru_reset: inconsistent shapes")
+    with torch.cuda.device(h.device):
+        _check(load().oflow_gru_reset_f32(pz, sz, br.data_ptr(), ph, sh, pr, sr, h.shape[0], ch, p, _stream(h.device)), "gru_reset")
+
+
+def gru_blend_(zr: torch.Tensor, bz: torch.Tensor, q: torch.Tensor, bq: torch.Tensor, h: torch.Tensor) -> None:
+    """h <- (1 - z) * h + z * tanh(q + bq), z = sigmoid(zr[:, :CH] + bz), in place."""
+    pz, sz, c2, p = _chan_view(zr, "gru_blend zr")
+    pq, sq, cq, p1 = _chan_view(q, "gru_blend q")
+    ph, sh, ch, p2 = _chan_view(h, "gru_blend h")
+    if c2 != 2 * ch or cq != ch or p1 != p or p2 != p or bz.numel() != ch or bq.numel() != ch:
+        raise RuntimeError("gru_blend: inconsistent shapes")
+    with torch.cuda.device(h.device):
+        _check(
+            load().oflow_gru_blend_f32(pz, sz, bz.data_ptr(), pq, sq, bq.data_ptr(), ph, sh, h.shape[0], ch, p, _stream(h.device)),
+            "gru_blend",
+        )
