@@ -79,6 +79,21 @@ int oflow_corr_lookup_f32(const float* const* d_levels, const int* level_h, cons
                           float* d_out, void* stream);
 
 /*
+ * Tiled pyramid storage (what CorrBlock uses internally): level l of each query is stored as
+ * [ceil(H_l/4)][ceil(W_l/8)][4][8] fp32 tiles, one 4x8 tile = one 128-B line, so a (2r+2)^2 lookup window
+ * touches ~7 lines instead of ~13 with canonical rows. oflow_corr_tiled_level_floats(H_l, W_l) = floats per query
+ * of a level; levels are otherwise produced and read exactly like the canonical ones above, and
+ * oflow_corr_untile_f32 rebuilds the canonical (Q, H_l, W_l) view bit-for-bit.
+ */
+long long oflow_corr_tiled_level_floats(int H_l, int W_l);
+int oflow_corr_pyramid_tiled_f32(const float* d_fmap1, const float* d_fmap2, int B, int C, int H, int W,
+                                 int num_levels, float* const* d_levels, void* stream);
+int oflow_corr_lookup_tiled_f32(const float* const* d_levels, const int* level_h, const int* level_w,
+                                int num_levels, const float* d_coords, int B, int H, int W, int radius,
+                                float* d_out, void* stream);
+int oflow_corr_untile_f32(const float* d_tiled, float* d_out, long long Q, int H_l, int W_l, void* stream);
+
+/*
  * Inverse warp (optical_flow.warp): out = grid_sample(frame, linspace-grid + flow, mode, padding_mode,
  * align_corners). d_frame, d_out: (B, C, H, W); d_flow: (B, 2, H, W) already normalized to [-1, 1] units.
  */

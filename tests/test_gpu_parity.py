@@ -254,3 +254,45 @@ def test_ops_follow_the_current_stream():
     s.synchronize()
     ref = ocorr.corr_lookup(ocorr.corr_pyramid(f1, f2, 4), ocorr.coords_grid(1, 24, 32), 4)
     assert (out.cpu() - ref).abs().max().item() <= 1e-4
+
+
+# ----------------------------------------------------------------------------------------------------------
+# tiled layout (what CorrBlock uses): must be a pure re-addressing of the canonical kernels' results
+# ----------------------------------------------------------------------------------------------------------
+@pytest.mark.parametrize("shape,levels", [((1, 256, 23, 37), 4), ((2, 64, 16, 20), 4), ((1, 256, 33, 70), 6), ((2, 256, 55, 128), 4)])
+def test_tiled_pyramid_untiles_to_canonical_bit_exact(shape, levels):
+    b, c, h, w = shape
+    f1, f2 = synthetic.synthetic_fmaps(b, c, h, w, stream=61 + c)
+    f1, f2 = f1.to(DEV), f2.to(DEV)
+    tp = _native.corr_pyramid_tiled(f1, f2, levels)
+    cp = _native.corr_pyramid(f1, f2, levels)
+    for lvl in range(levels):
+        assert torch.equal(tp.untile(lvl), cp[lvl]), lvl
+
+
+@pytest.mark.parametrize("radius", [0, 2, 4, 7])
+@pytest.mark.parametrize("sigma", [0.0, 4.0, 40.0])
+def test_tiled_lookup_equals_canonical_lookup(radius, sigma):
+    b, h, w = 2, 47, 156  # KITTI 1/8 grid: W_l not multiples of 8 at any level
+    f1, f2 = synthetic.synthetic_fmaps(b, 256, h, w, stream=63)
+    f1, f2 = f1.to(DEV), f2.to(DEV)
+    coords = (coords_grid(b, h, w) + torch.from_numpy(synthetic.hash_normal(64, (b, 2, h, w), sigma))).to(DEV)
+    tp = _native.corr_pyramid_tiled(f1, f2, 4)
+    cp = _native.corr_pyramid(f1, f2, 4)
+    assert torch.equal(_native.corr_lookup_tiled(tp, coords, radius), _native.corr_lookup(cp, coords, radius))
+
+
+def test_corrblock_pyramid_attribute_semantics():
+    """corr_pyramid reads as the reference's list; after access (or assignment) lookups follow that list."""
+    f1, f2 = synthetic.synthetic_fmaps(1, 64, 16, 16, stream=65)
+    cb = CorrBlock(f1.to(DEV), f2.to(DEV))
+    coords = coords_grid(1, 16, 16, device=DEV) + 0.5
+    before = cb(coords)
+    pyr = cb.corr_pyramid
+    assert [tuple(p.shape) for p in pyr] == [(256, 1, 16, 16), (256, 1, 8, 8), (256, 1, 4, 4), (256, 1, 2, 2)]
+    assert torch.equal(cb(coords), before)
+    pyr[0].zero_()
+    after = cb(coords)
+    assert torch.all(after[:, :81] == 0) and torch.equal(after[:, 81:], before[:, 81:])
+    cb.corr_pyramid = [p * 2 for p in pyr]
+    assert torch.equal(cb(coords)[:, 81:], 2 * before[:, 81:])

@@ -12,7 +12,7 @@ from optical_flow import _native
 
 def _declared_symbols():
     text = open(os.path.join(REPO, "include", "oflow.h")).read()
-    return sorted(set(re.findall(r"^\s*(?:const\s+)?\w+\**\s+\**(oflow_\w+)\s*\(", text, flags=re.M)))
+    return sorted(set(re.findall(r"^\s*(?:[\w*]+\s+)+\**(oflow_\w+)\s*\(", text, flags=re.M)))
 
 
 def test_header_and_binding_agree():

@@ -28,6 +28,8 @@ struct LookupArgs {
   const float* lv[OFLOW_MAX_LEVELS];
   int Hl[OFLOW_MAX_LEVELS];
   int Wl[OFLOW_MAX_LEVELS];
+  int HB[OFLOW_MAX_LEVELS];  // TILED: ceil(H_l / 4)
+  int WB[OFLOW_MAX_LEVELS];  // TILED: ceil(W_l / 8)
   const float* coords;  // (B, 2, N)
   float* out;           // (B, nlev*K*K, N)
   int N;                // query pixels per batch element
@@ -35,7 +37,9 @@ struct LookupArgs {
   int cout;             // nlev * K * K
 };
 
-template <int R>
+// TILED: level l stored as [q][H_l/4][W_l/8][4][8] (corr_pyramid.hip, lvl_off): one 4x8 tile = one 128-B line,
+// so a window's row segments share lines with the rows above/below them (fetched once into L2 by this workgroup).
+template <int R, bool TILED>
 __global__ __launch_bounds__(kThreads) void corr_lookup_kernel(LookupArgs a) {
   constexpr int PK = 2 * R + 2;   // patch side
   constexpr int K = 2 * R + 1;    // window side
@@ -54,6 +58,7 @@ __global__ __launch_bounds__(kThreads) void corr_lookup_kernel(LookupArgs a) {
   const int lvl = blockIdx.y;
   const int q0 = blockIdx.x * kQ;
   const int Hl = a.Hl[lvl], Wl = a.Wl[lvl];
+  const int HB = a.HB[lvl], WB = a.WB[lvl];
   const float* __restrict__ L = a.lv[lvl];
   const float inv = 1.0f / static_cast<float>(1 << lvl);  // exact power of two (corr.py:68)
 
@@ -98,7 +103,12 @@ __global__ __launch_bounds__(kThreads) void corr_lookup_kernel(LookupArgs a) {
       const int y = sY[q] + row, x = sX[q] + col;
       if (q0 + q < a.total && static_cast<unsigned>(y) < static_cast<unsigned>(Hl) &&
           static_cast<unsigned>(x) < static_cast<unsigned>(Wl))
-        v[s] = L[(size_t)(q0 + q) * (size_t)Hl * Wl + (size_t)y * Wl + x];
+      {
+        if constexpr (TILED)
+          v[s] = L[(((size_t)(q0 + q) * HB + (y >> 2)) * WB + (x >> 3)) * 32 + ((y & 3) << 3) + (x & 7)];
+        else
+          v[s] = L[(size_t)(q0 + q) * (size_t)Hl * Wl + (size_t)y * Wl + x];
+      }
     }
   }
 #pragma unroll
@@ -131,9 +141,12 @@ __global__ __launch_bounds__(kThreads) void corr_lookup_kernel(LookupArgs a) {
 }
 
 template <int R>
-int launch_lookup(const LookupArgs& a, int nlev, hipStream_t s) {
+int launch_lookup(const LookupArgs& a, int nlev, hipStream_t s, bool tiled) {
   dim3 grid((a.total + kQ - 1) / kQ, nlev);
-  hipLaunchKernelGGL(corr_lookup_kernel<R>, grid, dim3(kThreads), 0, s, a);
+  if (tiled)
+    hipLaunchKernelGGL((corr_lookup_kernel<R, true>), grid, dim3(kThreads), 0, s, a);
+  else
+    hipLaunchKernelGGL((corr_lookup_kernel<R, false>), grid, dim3(kThreads), 0, s, a);
   return launch_status();
 }
 
@@ -142,9 +155,9 @@ int launch_lookup(const LookupArgs& a, int nlev, hipStream_t s) {
 
 using namespace oflow;
 
-extern "C" int oflow_corr_lookup_f32(const float* const* d_levels, const int* level_h, const int* level_w,
-                                     int num_levels, const float* d_coords, int B, int H, int W, int radius,
-                                     float* d_out, void* stream) {
+static int corr_lookup_impl(const float* const* d_levels, const int* level_h, const int* level_w, int num_levels,
+                            const float* d_coords, int B, int H, int W, int radius, float* d_out, void* stream,
+                            bool tiled) {
   if (!d_levels || !level_h || !level_w || !d_coords || !d_out) return OFLOW_E_NULL;
   if (B <= 0 || H <= 0 || W <= 0) return OFLOW_E_SHAPE;
   if (num_levels < 1 || num_levels > OFLOW_MAX_LEVELS) return OFLOW_E_LEVELS;
@@ -158,6 +171,8 @@ extern "C" int oflow_corr_lookup_f32(const float* const* d_levels, const int* le
     a.lv[l] = d_levels[l];
     a.Hl[l] = level_h[l];
     a.Wl[l] = level_w[l];
+    a.HB[l] = (level_h[l] + 3) / 4;
+    a.WB[l] = (level_w[l] + 7) / 8;
   }
   const int K = 2 * radius + 1;
   a.coords = d_coords;
@@ -167,14 +182,26 @@ extern "C" int oflow_corr_lookup_f32(const float* const* d_levels, const int* le
   a.cout = num_levels * K * K;
   hipStream_t s = static_cast<hipStream_t>(stream);
   switch (radius) {
-    case 0: return launch_lookup<0>(a, num_levels, s);
-    case 1: return launch_lookup<1>(a, num_levels, s);
-    case 2: return launch_lookup<2>(a, num_levels, s);
-    case 3: return launch_lookup<3>(a, num_levels, s);
-    case 4: return launch_lookup<4>(a, num_levels, s);
-    case 5: return launch_lookup<5>(a, num_levels, s);
-    case 6: return launch_lookup<6>(a, num_levels, s);
-    case 7: return launch_lookup<7>(a, num_levels, s);
+    case 0: return launch_lookup<0>(a, num_levels, s, tiled);
+    case 1: return launch_lookup<1>(a, num_levels, s, tiled);
+    case 2: return launch_lookup<2>(a, num_levels, s, tiled);
+    case 3: return launch_lookup<3>(a, num_levels, s, tiled);
+    case 4: return launch_lookup<4>(a, num_levels, s, tiled);
+    case 5: return launch_lookup<5>(a, num_levels, s, tiled);
+    case 6: return launch_lookup<6>(a, num_levels, s, tiled);
+    case 7: return launch_lookup<7>(a, num_levels, s, tiled);
     default: return OFLOW_E_RADIUS;
   }
+}
+
+extern "C" int oflow_corr_lookup_f32(const float* const* d_levels, const int* level_h, const int* level_w,
+                                     int num_levels, const float* d_coords, int B, int H, int W, int radius,
+                                     float* d_out, void* stream) {
+  return corr_lookup_impl(d_levels, level_h, level_w, num_levels, d_coords, B, H, W, radius, d_out, stream, false);
+}
+
+extern "C" int oflow_corr_lookup_tiled_f32(const float* const* d_levels, const int* level_h, const int* level_w,
+                                           int num_levels, const float* d_coords, int B, int H, int W, int radius,
+                                           float* d_out, void* stream) {
+  return corr_lookup_impl(d_levels, level_h, level_w, num_levels, d_coords, B, H, W, radius, d_out, stream, true);
 }

@@ -37,6 +37,7 @@ struct PyramidArgs {
   float* lv[4];
   int C, H, W, N;
   int Hl[4], Wl[4];
+  int HB[4], WB[4];  // tiled layout: tile rows / cols per level (ceil(H_l/4), ceil(W_l/8))
   int nlev;         // levels written by the fused kernel (1..4)
   int tiles_x;      // ceil(W / 32)
   float scale;      // sqrt(C) as torch computes it (float sqrt of float(C))
@@ -111,7 +112,18 @@ struct Stage {
   }
 };
 
-template <bool VEC>
+// Offset of (query q, row y, col x) in level l: canonical (q, H_l, W_l) rows, or TILED [q][H_l/4][W_l/8][4][8]
+// (one 4x8 tile = one 128-B line: a (2r+2)^2 lookup window then touches ~7 lines instead of ~13).
+template <bool TILED>
+__device__ __forceinline__ size_t lvl_off(const PyramidArgs& p, int l, size_t q, int y, int x) {
+  if constexpr (TILED) {
+    return ((q * p.HB[l] + (y >> 2)) * p.WB[l] + (x >> 3)) * 32 + ((y & 3) << 3) + (x & 7);
+  } else {
+    return q * (size_t)(p.Hl[l] * p.Wl[l]) + (size_t)y * p.Wl[l] + x;
+  }
+}
+
+template <bool VEC, bool TILED>
 __global__ __launch_bounds__(kThreads, 2) void corr_pyramid_kernel(PyramidArgs p) {
   __shared__ __attribute__((aligned(16))) float sA[2][kBK][kBM];
   __shared__ __attribute__((aligned(16))) float sB[2][kBK][kBN];
@@ -175,7 +187,7 @@ __global__ __launch_bounds__(kThreads, 2) void corr_pyramid_kernel(PyramidArgs p
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int i = qbase + (r & 3) + 8 * (r >> 2);
-        if (ok && i < p.N) L0[((size_t)b * Nn + i) * Nn + (size_t)gy * p.W + gx] = acc[n][r];
+        if (ok && i < p.N) L0[lvl_off<TILED>(p, 0, (size_t)b * Nn + i, gy, gx)] = acc[n][r];
       }
     }
   }
@@ -201,7 +213,7 @@ __global__ __launch_bounds__(kThreads, 2) void corr_pyramid_kernel(PyramidArgs p
         const float a0 = acc[2 * m][r], c0 = acc[2 * m + 1][r];
         v1[h][r] = pool4(a0, dpp_xor1(a0), c0, dpp_xor1(c0));
         const int i = qbase + (r & 3) + 8 * (r >> 2);
-        if (ok && i < p.N) p.lv[1][((size_t)b * Nn + i) * (size_t)(H1 * W1) + (size_t)y1 * W1 + x1] = v1[h][r];
+        if (ok && i < p.N) p.lv[1][lvl_off<TILED>(p, 1, (size_t)b * Nn + i, y1, x1)] = v1[h][r];
       }
     }
     if (p.nlev >= 3) {
@@ -212,7 +224,7 @@ __global__ __launch_bounds__(kThreads, 2) void corr_pyramid_kernel(PyramidArgs p
         const float a0 = v1[0][r], c0 = v1[1][r];
         v2[pr][r] = pool4(a0, dpp_xor2(a0), c0, dpp_xor2(c0));
         const int i = qbase + (r & 3) + 8 * (r >> 2);
-        if (ok && i < p.N) p.lv[2][((size_t)b * Nn + i) * (size_t)(H2 * W2) + (size_t)y2 * W2 + x2] = v2[pr][r];
+        if (ok && i < p.N) p.lv[2][lvl_off<TILED>(p, 2, (size_t)b * Nn + i, y2, x2)] = v2[pr][r];
       }
     }
   }
@@ -227,7 +239,7 @@ __global__ __launch_bounds__(kThreads, 2) void corr_pyramid_kernel(PyramidArgs p
       const float a0 = v2[0][r], c0 = v2[1][r];
       const float v3 = pool4(a0, swz_xor4(a0), c0, swz_xor4(c0));
       const int i = qbase + (r & 3) + 8 * (r >> 2);
-      if (ok && i < p.N) p.lv[3][((size_t)b * Nn + i) * (size_t)(H3 * W3) + (size_t)y3 * W3 + x3] = v3;
+      if (ok && i < p.N) p.lv[3][lvl_off<TILED>(p, 3, (size_t)b * Nn + i, y3, x3)] = v3;
     }
   }
 }
@@ -246,10 +258,52 @@ __global__ __launch_bounds__(256) void avgpool2x2_kernel(const float* __restrict
   }
 }
 
+// tiled level -> canonical (q, H, W) rows (the reference's corr_pyramid[l] view)
+__global__ __launch_bounds__(256) void untile_kernel(const float* __restrict__ in, float* __restrict__ out, long long Q,
+                                                      int H, int W, int HB, int WB) {
+  const long long total = Q * H * W;
+  for (long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x; t < total; t += (long long)gridDim.x * blockDim.x) {
+    const long long q = t / ((long long)H * W);
+    const int rem = (int)(t - q * H * W);
+    const int y = rem / W, x = rem - y * W;
+    out[t] = in[((q * HB + (y >> 2)) * WB + (x >> 3)) * 32 + ((y & 3) << 3) + (x & 7)];
+  }
+}
+
+// tiled floor 2x2 pool for levels >= 4
+__global__ __launch_bounds__(256) void avgpool2x2_tiled_kernel(const float* __restrict__ in, float* __restrict__ out,
+                                                                long long planes, int HBi, int WBi, int Hout, int Wout,
+                                                                int HBo, int WBo) {
+  const long long total = planes * Hout * Wout;
+  for (long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x; t < total; t += (long long)gridDim.x * blockDim.x) {
+    const long long q = t / ((long long)Hout * Wout);
+    const int rem = (int)(t - q * Hout * Wout);
+    const int y = rem / Wout, x = rem - y * Wout;
+    auto at = [&](int yy, int xx) { return in[((q * HBi + (yy >> 2)) * WBi + (xx >> 3)) * 32 + ((yy & 3) << 3) + (xx & 7)]; };
+    out[((q * HBo + (y >> 2)) * WBo + (x >> 3)) * 32 + ((y & 3) << 3) + (x & 7)] =
+        pool4(at(2 * y, 2 * x), at(2 * y, 2 * x + 1), at(2 * y + 1, 2 * x), at(2 * y + 1, 2 * x + 1));
+  }
+}
+
 }  // namespace
 }  // namespace oflow
 
 using namespace oflow;
+
+extern "C" long long oflow_corr_tiled_level_floats(int H_l, int W_l) {
+  if (H_l <= 0 || W_l <= 0) return 0;
+  return (long long)((H_l + 3) / 4) * ((W_l + 7) / 8) * 32;
+}
+
+extern "C" int oflow_corr_untile_f32(const float* d_tiled, float* d_out, long long Q, int H_l, int W_l, void* stream) {
+  if (!d_tiled || !d_out) return OFLOW_E_NULL;
+  if (Q <= 0 || H_l <= 0 || W_l <= 0) return OFLOW_E_SHAPE;
+  const long long total = Q * H_l * W_l;
+  const long long want = (total + 255) / 256;
+  hipLaunchKernelGGL(untile_kernel, dim3((unsigned)(want < 16384 ? want : 16384)), dim3(256), 0,
+                     static_cast<hipStream_t>(stream), d_tiled, d_out, Q, H_l, W_l, (H_l + 3) / 4, (W_l + 7) / 8);
+  return launch_status();
+}
 
 extern "C" int oflow_corr_pyramid_dims(int H, int W, int num_levels, int* level_h, int* level_w) {
   if (!level_h || !level_w) return OFLOW_E_NULL;
@@ -265,11 +319,11 @@ extern "C" int oflow_corr_pyramid_dims(int H, int W, int num_levels, int* level_
   return OFLOW_OK;
 }
 
-extern "C" int oflow_corr_pyramid_f32(const float* d_fmap1, const float* d_fmap2, int B, int C, int H, int W,
-                                      int num_levels, float* const* d_levels, void* stream) {
+static int corr_pyramid_impl(const float* d_fmap1, const float* d_fmap2, int B, int C, int H, int W, int num_levels,
+                             float* const* d_levels, void* stream, bool tiled) {
   if (!d_fmap1 || !d_fmap2 || !d_levels) return OFLOW_E_NULL;
   if (B <= 0 || C <= 0 || H <= 0 || W <= 0) return OFLOW_E_SHAPE;
-  if ((long long)H * W > (1ll << 30) / 1) return OFLOW_E_SHAPE;
+  if ((long long)H * W > (1ll << 30)) return OFLOW_E_SHAPE;
   int hl[OFLOW_MAX_LEVELS], wl[OFLOW_MAX_LEVELS];
   int st = oflow_corr_pyramid_dims(H, W, num_levels, hl, wl);
   if (st != OFLOW_OK) return st;
@@ -293,6 +347,8 @@ extern "C" int oflow_corr_pyramid_f32(const float* d_fmap1, const float* d_fmap2
     p.lv[l] = l < num_levels ? d_levels[l] : nullptr;
     p.Hl[l] = l < num_levels ? hl[l] : 1;
     p.Wl[l] = l < num_levels ? wl[l] : 1;
+    p.HB[l] = (p.Hl[l] + 3) / 4;
+    p.WB[l] = (p.Wl[l] + 7) / 8;
   }
   p.tiles_x = (W + kTC - 1) / kTC;
   p.scale = sqrtf(static_cast<float>(C));
@@ -305,21 +361,34 @@ extern "C" int oflow_corr_pyramid_f32(const float* d_fmap1, const float* d_fmap2
   dim3 grid(p.tiles_x * tiles_y, (p.N + kBM - 1) / kBM, B);
   const bool vec = (W % 4 == 0) &&
                    (((reinterpret_cast<uintptr_t>(d_fmap1) | reinterpret_cast<uintptr_t>(d_fmap2)) & 15) == 0);
-  if (vec) {
-    hipLaunchKernelGGL(corr_pyramid_kernel<true>, grid, dim3(kThreads), 0, s, p);
-  } else {
-    hipLaunchKernelGGL(corr_pyramid_kernel<false>, grid, dim3(kThreads), 0, s, p);
-  }
+  if (vec && tiled) hipLaunchKernelGGL((corr_pyramid_kernel<true, true>), grid, dim3(kThreads), 0, s, p);
+  else if (vec) hipLaunchKernelGGL((corr_pyramid_kernel<true, false>), grid, dim3(kThreads), 0, s, p);
+  else if (tiled) hipLaunchKernelGGL((corr_pyramid_kernel<false, true>), grid, dim3(kThreads), 0, s, p);
+  else hipLaunchKernelGGL((corr_pyramid_kernel<false, false>), grid, dim3(kThreads), 0, s, p);
   st = launch_status();
   if (st != OFLOW_OK) return st;
   for (int l = 4; l < num_levels; ++l) {
     const long long planes = (long long)B * p.N;
     const long long total = planes * hl[l] * wl[l];
     const int blocks = (int)((total + 255) / 256 < 8192 ? (total + 255) / 256 : 8192);
-    hipLaunchKernelGGL(avgpool2x2_kernel, dim3(blocks), dim3(256), 0, s, d_levels[l - 1], d_levels[l], planes,
-                       hl[l - 1], wl[l - 1], hl[l], wl[l]);
+    if (tiled)
+      hipLaunchKernelGGL(avgpool2x2_tiled_kernel, dim3(blocks), dim3(256), 0, s, d_levels[l - 1], d_levels[l], planes,
+                         (hl[l - 1] + 3) / 4, (wl[l - 1] + 7) / 8, hl[l], wl[l], (hl[l] + 3) / 4, (wl[l] + 7) / 8);
+    else
+      hipLaunchKernelGGL(avgpool2x2_kernel, dim3(blocks), dim3(256), 0, s, d_levels[l - 1], d_levels[l], planes,
+                         hl[l - 1], wl[l - 1], hl[l], wl[l]);
     st = launch_status();
     if (st != OFLOW_OK) return st;
   }
   return OFLOW_OK;
+}
+
+extern "C" int oflow_corr_pyramid_f32(const float* d_fmap1, const float* d_fmap2, int B, int C, int H, int W,
+                                      int num_levels, float* const* d_levels, void* stream) {
+  return corr_pyramid_impl(d_fmap1, d_fmap2, B, C, H, W, num_levels, d_levels, stream, false);
+}
+
+extern "C" int oflow_corr_pyramid_tiled_f32(const float* d_fmap1, const float* d_fmap2, int B, int C, int H, int W,
+                                            int num_levels, float* const* d_levels, void* stream) {
+  return corr_pyramid_impl(d_fmap1, d_fmap2, B, C, H, W, num_levels, d_levels, stream, true);
 }

@@ -1,17 +1,19 @@
 """``CorrBlock`` drop-in (reference: methods/raft/model/corr.py:37-87) on the gfx950 kernels.
 
-* ``__init__`` — one launch of ``oflow_corr_pyramid_f32``: fp32 MFMA all-pairs volume with the 1/sqrt(C) scale
-  and the floor 2x2 average-pool levels fused into the GEMM epilogue (`corr.py:38-54, 79-87`).
-* ``__call__`` — one launch of ``oflow_corr_lookup_f32`` for all levels: the (2r+1)^2 bilinear window per level,
-  written straight into the (B, L*(2r+1)^2, H, W) fp32 NCHW output (`corr.py:56-77`, `utils.py:64-80`).
+* ``__init__`` — one launch of ``oflow_corr_pyramid_tiled_f32``: fp32 MFMA all-pairs volume with the 1/sqrt(C)
+  scale and the floor 2x2 average-pool levels fused into the GEMM epilogue (`corr.py:38-54, 79-87`), stored in
+  4x8 tiles (one 128-B line each) so that lookups touch about half the memory lines of row-major storage.
+* ``__call__`` — one launch of ``oflow_corr_lookup_tiled_f32`` for all levels: the (2r+1)^2 bilinear window per
+  level, written straight into the (B, L*(2r+1)^2, H, W) fp32 NCHW output (`corr.py:56-77`, `utils.py:64-80`).
 
 Attributes match the reference: ``num_levels``, ``radius`` and ``corr_pyramid`` (list of (B*H*W, 1, H_l, W_l)
-fp32 tensors; here views of one allocation). Divergence (documented): where a level is under 2 px in
+fp32 tensors), the latter rebuilt bit-exactly from the tiles on first access (after which lookups use it, so
+in-place edits to it behave as in the reference). Divergence (documented): where a level is under 2 px in
 H or W the reference returns NaN (it divides by W_l-1); this build raises ``ValueError`` at lookup time.
 """
 from __future__ import annotations
 
-from typing import List
+from typing import List, Optional
 
 from torch import Tensor
 
@@ -22,10 +24,28 @@ class CorrBlock:
     def __init__(self, fmap1: Tensor, fmap2: Tensor, num_levels: int = 4, radius: int = 4) -> None:
         self.num_levels = num_levels
         self.radius = radius
-        self.corr_pyramid: List[Tensor] = _native.corr_pyramid(fmap1, fmap2, num_levels)
+        # lookups read the tiled layout (4x8 tiles = 128-B lines); the canonical list is built on first access
+        self._tiled = _native.corr_pyramid_tiled(fmap1, fmap2, num_levels)
+        self._pyramid: Optional[List[Tensor]] = None
+
+    @property
+    def corr_pyramid(self) -> List[Tensor]:
+        """The reference's ``corr_pyramid``: (B*H*W, 1, H_l, W_l) fp32 per level. Materialised on first access;
+        from then on lookups read these tensors, so in-place edits behave as in the reference."""
+        if self._pyramid is None:
+            self._pyramid = [self._tiled.untile(l) for l in range(len(self._tiled.levels))]
+            self._tiled = None
+        return self._pyramid
+
+    @corr_pyramid.setter
+    def corr_pyramid(self, levels: List[Tensor]) -> None:
+        self._pyramid = list(levels)
+        self._tiled = None
 
     def __call__(self, coords: Tensor) -> Tensor:
-        return _native.corr_lookup(self.corr_pyramid, coords, self.radius)
+        if self._tiled is not None:
+            return _native.corr_lookup_tiled(self._tiled, coords, self.radius)
+        return _native.corr_lookup(self._pyramid, coords, self.radius)
 
     @staticmethod
     def corr(fmap1: Tensor, fmap2: Tensor) -> Tensor:

@@ -33,6 +33,10 @@ SYMBOLS = (
     "oflow_corr_pyramid_dims",
     "oflow_corr_pyramid_f32",
     "oflow_corr_lookup_f32",
+    "oflow_corr_tiled_level_floats",
+    "oflow_corr_pyramid_tiled_f32",
+    "oflow_corr_lookup_tiled_f32",
+    "oflow_corr_untile_f32",
     "oflow_grid_warp_f32",
     "oflow_grid_sample_f32",
     "oflow_corr_otf_prepare_f16",
@@ -103,6 +107,14 @@ def load() -> ctypes.CDLL:
     lib.oflow_corr_pyramid_f32.argtypes = [P, P, I, I, I, I, I, PP, P]
     lib.oflow_corr_lookup_f32.restype = I
     lib.oflow_corr_lookup_f32.argtypes = [PP, IP, IP, I, P, I, I, I, I, P, P]
+    lib.oflow_corr_tiled_level_floats.restype = ctypes.c_longlong
+    lib.oflow_corr_tiled_level_floats.argtypes = [I, I]
+    lib.oflow_corr_pyramid_tiled_f32.restype = I
+    lib.oflow_corr_pyramid_tiled_f32.argtypes = [P, P, I, I, I, I, I, PP, P]
+    lib.oflow_corr_lookup_tiled_f32.restype = I
+    lib.oflow_corr_lookup_tiled_f32.argtypes = [PP, IP, IP, I, P, I, I, I, I, P, P]
+    lib.oflow_corr_untile_f32.restype = I
+    lib.oflow_corr_untile_f32.argtypes = [P, P, ctypes.c_longlong, I, I, P]
     lib.oflow_grid_warp_f32.restype = I
     lib.oflow_grid_warp_f32.argtypes = [P, P, I, I, I, I, I, I, I, P, P]
     lib.oflow_grid_sample_f32.restype = I
@@ -188,6 +200,85 @@ def corr_pyramid(fmap1: torch.Tensor, fmap2: torch.Tensor, num_levels: int = 4) 
             what,
         )
     return levels
+
+
+class TiledPyramid:
+    """Correlation pyramid in the tiled layout (include/oflow.h): level l is a (B*H*W, tiles_l*32) fp32 tensor,
+    all levels views of one allocation; ``dims[l] = (H_l, W_l)``."""
+
+    __slots__ = ("levels", "dims", "queries")
+
+    def __init__(self, levels, dims, queries):
+        self.levels, self.dims, self.queries = levels, dims, queries
+
+    def untile(self, l: int) -> torch.Tensor:
+        """Canonical (B*H*W, 1, H_l, W_l) copy of level l (the reference's corr_pyramid[l]), bit-exact."""
+        hl, wl = self.dims[l]
+        src = self.levels[l]
+        out = torch.empty((self.queries, 1, hl, wl), device=src.device, dtype=torch.float32)
+        if out.numel():
+            with torch.cuda.device(src.device):
+                _check(load().oflow_corr_untile_f32(src.data_ptr(), out.data_ptr(), self.queries, hl, wl, _stream(src.device)), "untile")
+        return out
+
+
+def corr_pyramid_tiled(fmap1: torch.Tensor, fmap2: torch.Tensor, num_levels: int = 4) -> TiledPyramid:
+    """The all-pairs correlation pyramid (same values as ``corr_pyramid``) in the tiled lookup layout."""
+    what = "corr_pyramid"
+    f1 = _gpu_f32(fmap1, "fmap1", what)
+    f2 = _gpu_f32(fmap2, "fmap2", what)
+    if f1.dim() != 4 or f1.shape != f2.shape:
+        raise RuntimeError(f"{what}: fmap1 {tuple(fmap1.shape)} and fmap2 {tuple(fmap2.shape)} must be equal (B, C, H, W)")
+    if f1.device != f2.device:
+        raise RuntimeError(f"{what}: fmap1 and fmap2 are on different devices")
+    b, c, h, w = f1.shape
+    dims = pyramid_dims(h, w, num_levels)
+    if any(hl < 1 or wl < 1 for hl, wl in dims):
+        raise RuntimeError(f"{what}: {num_levels} levels of 2x2 pooling need H, W >= {2 ** (num_levels - 1)}")
+    q = b * h * w
+    per = [int(load().oflow_corr_tiled_level_floats(hl, wl)) for hl, wl in dims]
+    buf = torch.empty(max(1, q * sum(per)), device=f1.device, dtype=torch.float32)
+    levels, off = [], 0
+    for n in per:
+        levels.append(buf[off : off + q * n].view(q, n))
+        off += q * n
+    if q:
+        ptrs = (ctypes.c_void_p * num_levels)(*[lv.data_ptr() for lv in levels])
+        with torch.cuda.device(f1.device), _Timed("corr_pyramid", f1.device):
+            _check(
+                load().oflow_corr_pyramid_tiled_f32(f1.data_ptr(), f2.data_ptr(), b, c, h, w, num_levels, ptrs, _stream(f1.device)),
+                what,
+            )
+    return TiledPyramid(levels, dims, q)
+
+
+def corr_lookup_tiled(pyr: TiledPyramid, coords: torch.Tensor, radius: int) -> torch.Tensor:
+    """``corr_lookup`` on a ``TiledPyramid``: (B, L*(2r+1)^2, H, W) fp32."""
+    what = "corr_lookup"
+    co = _gpu_f32(coords, "coords", what)
+    if co.dim() != 4 or co.shape[1] != 2:
+        raise RuntimeError(f"{what}: coords must be (B, 2, H, W), got {tuple(coords.shape)}")
+    b, _, h, w = co.shape
+    nl = len(pyr.levels)
+    if b * h * w != pyr.queries:
+        raise RuntimeError(f"{what}: coords {tuple(coords.shape)} do not match the pyramid's {pyr.queries} queries")
+    if not 0 <= int(radius) <= MAX_RADIUS:
+        raise RuntimeError(f"{what}: radius {radius} outside [0, {MAX_RADIUS}]")
+    if pyr.levels[0].device != co.device:
+        raise RuntimeError(f"{what}: pyramid and coords are on different devices")
+    k = 2 * int(radius) + 1
+    out = torch.empty((b, nl * k * k, h, w), device=co.device, dtype=torch.float32)
+    if out.numel() == 0:
+        return out
+    ptrs = (ctypes.c_void_p * nl)(*[t.data_ptr() for t in pyr.levels])
+    hs = (ctypes.c_int * nl)(*[d[0] for d in pyr.dims])
+    ws = (ctypes.c_int * nl)(*[d[1] for d in pyr.dims])
+    with torch.cuda.device(co.device), _Timed("corr_lookup", co.device):
+        _check(
+            load().oflow_corr_lookup_tiled_f32(ptrs, hs, ws, nl, co.data_ptr(), b, h, w, int(radius), out.data_ptr(), _stream(co.device)),
+            what,
+        )
+    return out
 
 
 def corr_lookup(levels: Sequence[torch.Tensor], coords: torch.Tensor, radius: int) -> torch.Tensor:
