@@ -58,7 +58,12 @@ def main():
     torch.cuda.empty_cache()
     pm = timed(lambda: _native.corr_pyramid(f1, f2, 4), args.iters)
     pyr = _native.corr_pyramid(f1, f2, 4)
-    lm = timed(lambda: _native.corr_lookup(pyr, coords, 4), args.iters * 5)
+    lm_canon = timed(lambda: _native.corr_lookup(pyr, coords, 4), args.iters * 5)
+    del pyr
+    torch.cuda.empty_cache()
+    pmt = timed(lambda: _native.corr_pyramid_tiled(f1, f2, 4), args.iters)
+    tp = _native.corr_pyramid_tiled(f1, f2, 4)
+    lm = timed(lambda: _native.corr_lookup_tiled(tp, coords, 4), args.iters * 5)
     # warp operator at the SURVEY §8(d) shape: frame (8, 3, 436, 1024), flow = normalize(N(0, 8^2) px)
     import optical_flow
     frame, _ = synthetic.synthetic_pair(8, 436, 1024, seed=1)
@@ -75,7 +80,10 @@ def main():
                 "pyramid_ms": round(pm, 4),
                 "pyramid_tflops": round(flops / pm / 1e9, 2),
                 "pyramid_GBs": round(pbytes / pm / 1e6, 1),
+                "pyramid_tiled_ms": round(pmt, 4),
                 "lookup_ms": round(lm, 5),
+                "lookup_canonical_ms": round(lm_canon, 5),
+                "lookup_canonical_GBs": round(lb / lm_canon / 1e6, 1),
                 "lookup_GBs": round(lb / lm / 1e6, 1),
                 "lookup_bytes": lb,
                 "warp_ms": round(wm, 5),
