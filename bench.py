@@ -107,8 +107,8 @@ def main() -> int:
     ap.add_argument("--pairs-per-gpu", type=int, default=None)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-events", action="store_true", help="do not record per-kernel HIP events")
-    ap.add_argument("--conv-benchmark", action="store_true", help="torch.backends.cudnn.benchmark (MIOpen exhaustive find)")
-    ap.add_argument("--channels-last", action="store_true", help="run the encoders / update block in NHWC")
+    ap.add_argument("--no-conv-benchmark", action="store_true",
+                    help="disable torch.backends.cudnn.benchmark (MIOpen exhaustive find of the conv algorithms)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -130,12 +130,10 @@ def main() -> int:
     ppg = args.pairs_per_gpu or ppg
     global_batch = ppg * world
 
-    torch.backends.cudnn.benchmark = bool(args.conv_benchmark)
+    torch.backends.cudnn.benchmark = not args.no_conv_benchmark
     model = RAFT(alternate_corr=alt).eval()
     model.load_state_dict(synthetic.synthetic_state_dict(model.state_dict()))
     model = model.to(dev)
-    if args.channels_last:
-        model = model.to(memory_format=torch.channels_last)
 
     img0 = img1 = None
     if args.workload == "corr":  # configs[1]: fmaps (B, 256, 128, 128) ~ N(0, 1.45^2), coords = grid + N(0, 4^2)
@@ -162,9 +160,6 @@ def main() -> int:
 
     def forward(s0, s1):
         p0, p1 = padder.pad(s0, s1)
-        if args.channels_last:
-            p0 = p0.contiguous(memory_format=torch.channels_last)
-            p1 = p1.contiguous(memory_format=torch.channels_last)
         low, up = model(p0, p1, iters=iters, test_mode=True)
         return low, padder.unpad(up)
 
@@ -224,8 +219,7 @@ def main() -> int:
             "iters": iters,
             "padded": f"{dims[0][0] * 8}x{dims[0][1] * 8}",
             "parallelism": f"pairs sharded over {world} GPU(s)" + (", RCCL scatter/gather" if world > 1 else ""),
-            "conv_benchmark": bool(args.conv_benchmark),
-            "channels_last": bool(args.channels_last),
+            "conv_benchmark": not args.no_conv_benchmark,
         },
     }
     if rec and alt:

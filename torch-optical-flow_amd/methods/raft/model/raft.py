@@ -11,7 +11,8 @@ values; three output-identical changes remove host work from the loop:
   * with ``test_mode=True`` only the last iteration's convex upsampling is computed — the reference computes
     all ``iters`` and returns only the last (Q11, `raft.py:136-145`);
   * without autograd on the GPU the update block runs through ``FusedUpdate`` (fused bias/activation/GRU
-    elementwise kernels over persistent concatenated buffers; same weights and arithmetic up to rounding).
+    elementwise kernels over persistent concatenated buffers; same weights and arithmetic up to rounding), and in
+    test mode its mask head (two convolutions feeding only the upsampling) runs at the last iteration only.
 """
 from __future__ import annotations
 
@@ -158,12 +159,14 @@ class RAFT(nn.Module):
             coords1 = coords1.detach()
             corr = corr_fn(coords1)
             flow = coords1 - coords0
+            last = itr == iters - 1
             if runner is not None:
-                net, up_mask, delta_flow = runner.step(corr, flow)
+                # Q11: in test mode only the last iteration's mask (upsampling) is ever used
+                net, up_mask, delta_flow = runner.step(corr, flow, need_mask=not test_mode or last)
             else:
                 net, up_mask, delta_flow = self.update_block(net, inp, corr, flow)
             coords1 = coords1 + delta_flow
-            if test_mode and itr != iters - 1:
+            if test_mode and not last:
                 continue  # Q11: intermediate upsamplings are never returned in test mode
             if up_mask is None:
                 flow_up = upflow8(coords1 - coords0)

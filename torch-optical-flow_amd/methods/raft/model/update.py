@@ -6,7 +6,7 @@ the reference's. ``ConvGRU`` (unused by RAFT) is not provided.
 """
 from __future__ import annotations
 
-from typing import Tuple
+from typing import Optional, Tuple
 
 import torch
 import torch.nn as nn
@@ -128,7 +128,9 @@ class FusedUpdate:
     def _conv(x: Tensor, conv: nn.Conv2d) -> Tensor:
         return F.conv2d(x, conv.weight, None, conv.stride, conv.padding, conv.dilation, conv.groups)
 
-    def step(self, corr: Tensor, flow: Tensor) -> Tuple[Tensor, Tensor, Tensor]:
+    def step(self, corr: Tensor, flow: Tensor, need_mask: bool = True) -> Tuple[Tensor, Optional[Tensor], Tensor]:
+        """One update: returns (net, 0.25 * mask(net) or None when ``need_mask`` is False, delta_flow). The mask
+        head only feeds the convex upsampling, which test mode needs at the last iteration alone."""
         enc, blk = self.block.encoder, self.block
         cor = _native.bias_act_(self._conv(corr, enc.convc1), enc.convc1.bias, "relu")
         cor = _native.bias_act_(self._conv(cor, enc.convc2), enc.convc2.bias, "relu")
@@ -148,6 +150,8 @@ class FusedUpdate:
         net = h.contiguous()
         fh = blk.flow_head
         delta_flow = fh.conv2(_native.bias_act_(self._conv(net, fh.conv1), fh.conv1.bias, "relu"))
-        m = _native.bias_act_(self._conv(net, blk.mask[0]), blk.mask[0].bias, "relu")
-        mask = _native.bias_act_(self._conv(m, blk.mask[2]), blk.mask[2].bias, "none", scale=0.25)
+        mask = None
+        if need_mask:
+            m = _native.bias_act_(self._conv(net, blk.mask[0]), blk.mask[0].bias, "relu")
+            mask = _native.bias_act_(self._conv(m, blk.mask[2]), blk.mask[2].bias, "none", scale=0.25)
         return net, mask, delta_flow
