@@ -107,6 +107,8 @@ def main() -> int:
     ap.add_argument("--pairs-per-gpu", type=int, default=None)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-events", action="store_true", help="do not record per-kernel HIP events")
+    ap.add_argument("--conv-events", action="store_true", help="also time every update-block conv launch")
+    ap.add_argument("--update-impl", default="split", choices=["split", "fused", "module"])
     ap.add_argument("--no-conv-benchmark", action="store_true",
                     help="disable torch.backends.cudnn.benchmark (MIOpen exhaustive find of the conv algorithms)")
     args = ap.parse_args()
@@ -134,6 +136,7 @@ def main() -> int:
     model = RAFT(alternate_corr=alt).eval()
     model.load_state_dict(synthetic.synthetic_state_dict(model.state_dict()))
     model = model.to(dev)
+    model.update_impl = args.update_impl
 
     img0 = img1 = None
     if args.workload == "corr":  # configs[1]: fmaps (B, 256, 128, 128) ~ N(0, 1.45^2), coords = grid + N(0, 4^2)
@@ -174,7 +177,7 @@ def main() -> int:
         for _ in range(args.warmup):
             step()
         torch.cuda.synchronize(dev)
-        rec = {} if not args.no_events else None
+        rec = ({"*": True} if args.conv_events else {}) if not args.no_events else None
         _native.set_event_recorder(rec)
         if world > 1:
             dist.barrier()
@@ -209,7 +212,8 @@ def main() -> int:
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": "f16 features / f32 accumulate (corr); f32 elsewhere" if alt else "f32",
+        "dtype": ("f16 features / f32 accumulate (corr); " if alt else "f32 corr; ")
+        + ("update convs f32 as split-f16 hi+lo operands (3 MFMA/product, f32 accumulate)" if args.update_impl == "split" else "f32"),
         "data": "synthetic (integer texture frames with a known (3, -1.5) px shift; hash-initialised weights)",
         "config": {
             "workload": (f"corr-build+{iters}-lookups-fmaps-{ppg}x256x128x128" if args.workload == "corr"
@@ -220,8 +224,12 @@ def main() -> int:
             "padded": f"{dims[0][0] * 8}x{dims[0][1] * 8}",
             "parallelism": f"pairs sharded over {world} GPU(s)" + (", RCCL scatter/gather" if world > 1 else ""),
             "conv_benchmark": not args.no_conv_benchmark,
+            "update_impl": args.update_impl,
         },
     }
+    if rec and args.conv_events:
+        convs = {k: v for k, v in rec.items() if k.startswith("conv") or k == "flow_prep"}
+        line["conv_ms_per_step"] = {k: round(sum(a.elapsed_time(b) for a, b in v) / args.steps, 3) for k, v in convs.items()}
     if rec and alt:
         lk = rec.get("corr_lookup_otf", [])
         pp = rec.get("corr_otf_prepare", [])

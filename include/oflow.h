@@ -16,6 +16,7 @@
  *   oflow_corr_lookup_f32   <- methods/raft/model/corr.py:56-77 (CorrBlock.__call__)
  *                              + methods/raft/model/utils.py:64-80 (bilinear_sampler)
  *   oflow_grid_warp_f32     <- optical_flow/operator/operator.py:8-56 (warp, warp_grid -> F.grid_sample)
+ *   oflow_conv_s32 & co.    <- methods/raft/model/update.py:40-161 (update-block convolutions)
  */
 #ifndef OFLOW_H_
 #define OFLOW_H_
@@ -137,6 +138,46 @@ int oflow_gru_reset_f32(const float* d_zr, long long szr, const float* d_br, con
                         float* d_rh, long long srh, int B, int CH, int P, void* stream);
 int oflow_gru_blend_f32(const float* d_zr, long long szr, const float* d_bz, const float* d_q, long long sq,
                         const float* d_bq, float* d_h, long long sh, int B, int CH, int P, void* stream);
+
+/*
+ * Split-fp16 ("S32") update-block path: fp32-accurate convolutions on the fp16 matrix cores
+ * (methods/raft/model/update.py:40-161; csrc/conv_s32.hip).
+ *
+ * S32 activation format: NHWC by groups of 32 channels; element (pixel p, channel c) of a buffer with G groups
+ * is hi = fp16(v) at byte p*G*128 + (c/32)*128 + (c%32)*2 and lo = fp16(v - hi) 64 bytes further (v ~ hi + lo,
+ * 22 significant bits). A channel slice starting at group g0 is (base + g0*128, pixel stride G*128).
+ * Padding channels (beyond the real ones, up to a multiple of 32) must hold zeros.
+ *
+ * oflow_conv_s32: stride-1 'same' convolution, kernel kh x kw in {1x1, 3x3, 1x5, 5x1}, over in_groups*32 input
+ *   channels. d_wpack = weights packed as [in_groups][kh*kw][n_pad][hi[32] | lo[32]] fp16 after scaling output
+ *   channel n by 2^s_n (|w| <= 2^14); d_wscale[n] = 2^-s_n. block_n in {32, 64, 128} divides n_pad.
+ *   value = act(acc * wscale[n] + bias[n]) * out_scale, act 0 none, 1 relu, 2 sigmoid, 3 tanh, then
+ *   epilogue 0: stored to S32 d_y0 (and d_y1 if not NULL) for channels n < N, and/or to fp32 NCHW d_f32
+ *               (batch / channel strides in floats; f32_accumulate = 1 adds to it);
+ *   epilogue 1 (GRU gates, N = 2*CH): n < CH -> z = sigmoid(.) into d_gru_z ([P][CH] fp32);
+ *               n >= CH -> sigmoid(.) * d_gru_h[p][n-CH] into S32 d_y0 channel n-CH   (update.py:91-96)
+ *   epilogue 2 (GRU candidate, N = CH): h = (1 - z) * h + z * tanh(.), in place in d_gru_h and into S32 d_y0
+ *               (update.py:96-97). (act is ignored by epilogues 1 and 2.)
+ * oflow_pack_s32_f32: d_x (B, C, H, W) fp32 with batch stride x_batch_stride -> act -> S32 d_y0 (and d_y1), and
+ *   optionally a [P][nhwc_pixel_stride] fp32 copy.                       (raft.py:115-118: tanh / relu of cnet)
+ * oflow_flow_prep_s32: flow = coords1 - pixel grid (raft.py:129) as the 7x7 patch matrix of convf1
+ *   (d_patches: S32 with 4 groups; channel t*2 + c = flow c at tap t = ky*7 + kx, zero padded) and, if not NULL,
+ *   the 2 flow channels at d_flow0 / d_flow1 (byte address of the hi half of the x channel; y follows).
+ * oflow_corr_lookup_tiled_s32: oflow_corr_lookup_tiled_f32 written as S32 (d_out, out_pixel_stride bytes).
+ */
+int oflow_conv_s32(const void* d_x, long long x_pixel_stride, int in_groups, const void* d_wpack, int n_pad,
+                   const float* d_wscale, const float* d_bias, int N, int B, int H, int W, int kh, int kw, int block_n,
+                   int epilogue, int activation, float out_scale, void* d_y0, long long y0_pixel_stride, void* d_y1,
+                   long long y1_pixel_stride, float* d_f32, long long f32_batch_stride, long long f32_channel_stride,
+                   int f32_accumulate, float* d_gru_h, float* d_gru_z, int gru_channels, void* stream);
+int oflow_pack_s32_f32(const float* d_x, long long x_batch_stride, int C, int B, int H, int W, int activation,
+                       void* d_y0, long long y0_pixel_stride, void* d_y1, long long y1_pixel_stride, float* d_nhwc,
+                       int nhwc_pixel_stride, void* stream);
+int oflow_flow_prep_s32(const float* d_coords, int B, int H, int W, void* d_patches, void* d_flow0,
+                        long long flow0_pixel_stride, void* d_flow1, long long flow1_pixel_stride, void* stream);
+int oflow_corr_lookup_tiled_s32(const float* const* d_levels, const int* level_h, const int* level_w, int num_levels,
+                                const float* d_coords, int B, int H, int W, int radius, void* d_out,
+                                long long out_pixel_stride, void* stream);
 
 #ifdef __cplusplus
 }

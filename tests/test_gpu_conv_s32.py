@@ -1,0 +1,199 @@
+"""Split-fp16 ("S32") update-block kernels (csrc/conv_s32.hip, s32_io.hip) through the C ABI, against PyTorch.
+
+Reference for every convolution: ``F.conv2d`` in float64 on the exact operands the kernel sees (input = hi + lo of
+the S32 tensor, fp32 weights), plus the plain PyTorch fp32 convolution on the GPU. Tolerance: the kernel's error
+comes from representing weights and activations with 22 significant bits and fp32 accumulation; the bound used is
+|d| <= 2e-6 * sum|x||w| (the per-output absolute-product sum, computed by a float64 convolution of |x| and |w|)
++ 1e-6, i.e. a few fp32 roundings of the largest partial sums. Integer exactness: with small-integer operands
+(exact in fp16) the result must be exact, which pins the MFMA operand/accumulator lane maps (A = I checks with an
+asymmetric B, cdna_hip_programming.md §3).
+"""
+import math
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+from optical_flow import _native as N
+from model.corr import CorrBlock
+from model.utils import coords_grid
+
+pytestmark = pytest.mark.gpu
+DEV = torch.device("cuda", 0)
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _need_gpu():
+    assert torch.cuda.is_available(), "GPU tests need a ROCm GPU"
+    N.load()
+
+
+def _ref(x, w, b, kh, kw):
+    pad = (kh // 2, kw // 2)
+    y = F.conv2d(x.double(), w.double(), None if b is None else b.double(), padding=pad)
+    bound = F.conv2d(x.double().abs(), w.double().abs(), None, padding=pad)
+    return y, bound
+
+
+def _act(y, act):
+    return {"none": y, "relu": torch.relu(y), "sigmoid": torch.sigmoid(y), "tanh": torch.tanh(y)}[act]
+
+
+CASES = [
+    # kh, kw, cin, n, block_n, B, H, W
+    (1, 1, 352, 256, 128, 2, 13, 45),
+    (3, 3, 256, 192, 64, 2, 13, 45),
+    (3, 3, 128, 64, 64, 1, 7, 33),
+    (3, 3, 256, 126, 128, 2, 9, 40),
+    (3, 3, 256, 2, 32, 2, 11, 70),
+    (1, 5, 384, 256, 128, 2, 6, 37),
+    (5, 1, 384, 128, 128, 2, 10, 31),
+    (1, 1, 100, 96, 32, 1, 5, 64),
+    (3, 3, 128, 256, 128, 8, 55, 128),
+]
+
+
+@pytest.mark.parametrize("kh,kw,cin,n,bn,b,h,w", CASES)
+def test_conv_s32_matches_fp64(kh, kw, cin, n, bn, b, h, w):
+    g = torch.Generator().manual_seed(kh * 1000 + cin + n)
+    x = (torch.randn(b, cin, h, w, generator=g) * 1.5).to(DEV)
+    wt = (torch.randn(n, cin, kh, kw, generator=g) / math.sqrt(cin * kh * kw)).to(DEV)
+    bias = torch.randn(n, generator=g).to(DEV)
+    xs = N.s32_from_f32(x)
+    xr = N.s32_to_f32(xs, cin)
+    npad = ((n + bn - 1) // bn) * bn
+    cw = N.ConvWeights(wt, bias, npad)
+    out = N.s32_empty(b, h, w, (n + 31) // 32, DEV, zero=True)
+    f32 = torch.zeros(b, n, h, w, device=DEV)
+    N.conv_s32(N.S32Slice(xs), cw, bn, act="none", y0=N.S32Slice(out), f32=f32)
+    torch.cuda.synchronize()
+    ref, bound = _ref(xr, wt, bias, kh, kw)
+    tol = 2e-6 * bound + 1e-6
+    err = (f32.double() - ref).abs()
+    assert bool((err <= tol).all()), f"fp32 out: max err {float(err.max()):.3e}, worst ratio {float((err / tol).max()):.2f}"
+    got = N.s32_to_f32(out, n).double()
+    err2 = (got - ref).abs()
+    assert bool((err2 <= tol + 2.0 ** -22 * ref.abs()).all()), f"S32 out: max err {float(err2.max()):.3e}"
+    # the plain PyTorch fp32 convolution of the original input on the GPU
+    y32 = F.conv2d(x, wt, bias, padding=(kh // 2, kw // 2))
+    rel = float((f32 - y32).abs().max() / y32.abs().max())
+    assert rel <= 2e-6, rel
+
+
+@pytest.mark.parametrize("kh,kw", [(1, 1), (3, 3), (1, 5), (5, 1)])
+def test_conv_s32_integer_exact(kh, kw):
+    """Small-integer operands: every product and partial sum is exact, so the result must be bit-exact."""
+    g = torch.Generator().manual_seed(7 + kh * 10 + kw)
+    b, cin, n, h, w = 2, 64, 128, 9, 36
+    x = torch.randint(-8, 9, (b, cin, h, w), generator=g).float().to(DEV)
+    wt = torch.randint(-4, 5, (n, cin, kh, kw), generator=g).float().to(DEV)
+    wt[0] = 0
+    wt[0, 0, kh // 2, kw // 2] = 1  # output channel 0 = input channel 0 (identity row)
+    cw = N.ConvWeights(wt, None, 128)
+    f32 = torch.empty(b, n, h, w, device=DEV)
+    N.conv_s32(N.S32Slice(N.s32_from_f32(x)), cw, 128, f32=f32)
+    ref = F.conv2d(x.double(), wt.double(), padding=(kh // 2, kw // 2))
+    assert torch.equal(f32.double(), ref)
+    assert torch.equal(f32[:, 0], x[:, 0])
+
+
+def test_conv_s32_epilogues_slices_and_accumulate():
+    g = torch.Generator().manual_seed(3)
+    b, h, w = 2, 12, 40
+    x = torch.randn(b, 256, h, w, generator=g).to(DEV)
+    wt = (torch.randn(126, 256, 3, 3, generator=g) * 0.02).to(DEV)
+    bias = torch.randn(126, generator=g).to(DEV)
+    cw = N.ConvWeights(wt, bias, 128)
+    xs = N.s32_from_f32(x)
+    # destinations: channels 256..381 of two 12-group buffers; channels 382, 383 hold sentinels
+    d0 = N.s32_from_f32(torch.full((b, 384, h, w), 7.0, device=DEV))
+    d1 = d0.clone()
+    N.conv_s32(N.S32Slice(xs), cw, 128, act="relu", out_scale=0.5, y0=N.S32Slice(d0, 8, 4), y1=N.S32Slice(d1, 8, 4))
+    ref = _act(_ref(N.s32_to_f32(xs), wt, bias, 3, 3)[0], "relu") * 0.5
+    for d in (d0, d1):
+        got = N.s32_to_f32(d)
+        assert float((got[:, 256:382].double() - ref).abs().max()) <= 1e-4
+        assert bool((got[:, :256] == 7.0).all()) and bool((got[:, 382:] == 7.0).all())
+    # fp32 accumulate into a (B, 2, H, W) tensor (flow head -> coords += delta)
+    w2 = (torch.randn(2, 256, 3, 3, generator=g) * 0.02).to(DEV)
+    cw2 = N.ConvWeights(w2, torch.tensor([0.5, -0.25], device=DEV), 32)
+    coords = torch.randn(b, 2, h, w, device=DEV)
+    c0 = coords.clone()
+    N.conv_s32(N.S32Slice(xs), cw2, 32, f32=coords, f32_accumulate=True)
+    delta = F.conv2d(N.s32_to_f32(xs).double(), w2.double(), cw2.bias.double(), padding=1)
+    assert float((coords.double() - (c0.double() + delta)).abs().max()) <= 1e-5
+
+
+def test_conv_s32_gru_epilogues():
+    """z|r gates and the candidate/blend epilogue against the SepConvGRU math (update.py:91-97)."""
+    g = torch.Generator().manual_seed(11)
+    b, h, w, ch = 2, 8, 36, 128
+    hx = torch.randn(b, 384, h, w, generator=g).to(DEV)
+    hx[:, :ch] = torch.tanh(hx[:, :ch])
+    hmaster = hx[:, :ch].permute(0, 2, 3, 1).reshape(-1, ch).contiguous()
+    hx_s = N.s32_from_f32(hx)
+    rhx_s = hx_s.clone()
+    wz, wr, wq = ((torch.randn(ch, 384, 1, 5, generator=g) * 0.02).to(DEV) for _ in range(3))
+    bz, br, bq = (torch.randn(ch, generator=g).to(DEV) for _ in range(3))
+    czr = N.ConvWeights(torch.cat([wz, wr]), torch.cat([bz, br]), 256)
+    cq = N.ConvWeights(wq, bq, 128)
+    z = torch.empty(b * h * w, ch, device=DEV)
+    N.conv_s32(N.S32Slice(hx_s), czr, 128, epilogue=1, y0=N.S32Slice(rhx_s, 0, 4), gru_h=hmaster, gru_z=z)
+    hxr = N.s32_to_f32(hx_s).double()
+    zr_ref = torch.sigmoid(F.conv2d(hxr, wz.double(), bz.double(), padding=(0, 2)))
+    r_ref = torch.sigmoid(F.conv2d(hxr, wr.double(), br.double(), padding=(0, 2)))
+    zg = z.view(b, h, w, ch).permute(0, 3, 1, 2).double()
+    assert float((zg - zr_ref).abs().max()) <= 2e-6
+    rh_ref = r_ref * hx[:, :ch].double()
+    rhx = N.s32_to_f32(rhx_s).double()
+    assert float((rhx[:, :ch] - rh_ref).abs().max()) <= 2e-6
+    assert torch.equal(rhx[:, ch:], hxr[:, ch:])
+    h_ref = hx[:, :ch].double()
+    N.conv_s32(N.S32Slice(rhx_s), cq, 128, epilogue=2, y0=N.S32Slice(hx_s, 0, 4), gru_h=hmaster, gru_z=z)
+    q_ref = torch.tanh(F.conv2d(rhx, wq.double(), bq.double(), padding=(0, 2)))
+    hn_ref = (1 - zg) * h_ref + zg * q_ref
+    hn = hmaster.view(b, h, w, ch).permute(0, 3, 1, 2).double()
+    assert float((hn - hn_ref).abs().max()) <= 2e-6
+    assert float((N.s32_to_f32(hx_s)[:, :ch].double() - hn).abs().max()) <= 2.0 ** -21
+
+
+def test_pack_s32_and_flow_prep():
+    g = torch.Generator().manual_seed(5)
+    b, h, w = 2, 11, 29
+    cnet = torch.randn(b, 256, h, w, generator=g).to(DEV)
+    hx = N.s32_empty(b, h, w, 12, DEV, zero=True)
+    rhx = N.s32_empty(b, h, w, 12, DEV, zero=True)
+    hm = torch.empty(b * h * w, 128, device=DEV)
+    N.pack_s32(cnet[:, :128], "tanh", N.S32Slice(hx, 0, 4), nhwc=hm)
+    N.pack_s32(cnet[:, 128:], "relu", N.S32Slice(hx, 4, 4), N.S32Slice(rhx, 4, 4))
+    got = N.s32_to_f32(hx)
+    assert float((got[:, :128] - torch.tanh(cnet[:, :128])).abs().max()) <= 1e-6
+    assert torch.equal(hm.view(b, h, w, 128).permute(0, 3, 1, 2), torch.tanh(cnet[:, :128]))
+    assert float((got[:, 128:256] - torch.relu(cnet[:, 128:])).abs().max()) <= 2e-6 * float(cnet.abs().max())
+    assert torch.equal(N.s32_to_f32(rhx)[:, 128:256], got[:, 128:256])
+    coords = coords_grid(b, h, w, device=DEV) + torch.randn(b, 2, h, w, generator=g).to(DEV) * 5
+    pm = N.s32_empty(b, h, w, 4, DEV)
+    N.flow_prep(coords, pm, (N.S32Slice(hx), 382), (N.S32Slice(rhx), 382))
+    flow = coords - coords_grid(b, h, w, device=DEV)
+    unf = F.unfold(flow, 7, padding=3).view(b, 2, 49, h, w).permute(0, 2, 1, 3, 4).reshape(b, 98, h, w)
+    pmf = N.s32_to_f32(pm)
+    assert float((pmf[:, :98] - unf).abs().max()) <= 1e-6 * float(flow.abs().max())
+    assert bool((pmf[:, 98:] == 0).all())
+    for t in (hx, rhx):
+        assert float((N.s32_to_f32(t)[:, 382:] - flow).abs().max()) <= 1e-6 * float(flow.abs().max())
+
+
+@pytest.mark.parametrize("sigma", [0.0, 3.0, 25.0])
+def test_lookup_s32_equals_lookup(sigma):
+    g = torch.Generator().manual_seed(int(sigma) + 1)
+    b, c, h, w = 2, 256, 23, 37
+    f1 = torch.randn(b, c, h, w, generator=g).to(DEV)
+    f2 = torch.randn(b, c, h, w, generator=g).to(DEV)
+    pyr = N.corr_pyramid_tiled(f1, f2, 4)
+    coords = coords_grid(b, h, w, device=DEV) + torch.randn(b, 2, h, w, generator=g).to(DEV) * sigma
+    ref = N.corr_lookup_tiled(pyr, coords, 4)
+    out = N.s32_empty(b, h, w, 11, DEV, zero=True)
+    N.corr_lookup_tiled_s32(pyr, coords, 4, out)
+    got = N.s32_to_f32(out)
+    assert float((got[:, :324] - ref).abs().max()) <= 2.0 ** -21 * max(1.0, float(ref.abs().max()))
+    assert bool((got[:, 324:] == 0).all())

@@ -28,20 +28,22 @@ def _epe(a, b):
     return float(e.mean()), float(e.max())
 
 
+@pytest.mark.parametrize("impl", ["split", "fused"])
 @pytest.mark.parametrize("tag", ["small", "small24", "kittimode", "sintel", "kitti"])
-def test_raft_matches_reference_flows(golden, tag):
+def test_raft_matches_reference_flows(golden, tag, impl):
     g = golden("raft_e2e")
     b, h, w, iters, s, seed = (int(v) for v in g[f"{tag}_cfg"])
     img0, img1 = synthetic.synthetic_pair(b, h, w, seed=seed)
     padder = InputPadder(img0.shape, mode=str(g[f"{tag}_mode"]))
     p0, p1 = (x.to(DEV) for x in padder.pad(img0, img1))
     model = _model(RAFT)
+    model.update_impl = impl
     with torch.inference_mode():
         low, up = model(p0, p1, iters=iters, test_mode=True)
     up = padder.unpad(up)[..., ::s, ::s]
     ml, xl = _epe(low, g[f"{tag}_low"])
     mu, xu = _epe(up, g[f"{tag}_up"])
-    print(f"{tag}: low EPE mean {ml:.2e} max {xl:.2e}; up EPE mean {mu:.2e} max {xu:.2e}")
+    print(f"{tag} [{impl}]: low EPE mean {ml:.2e} max {xl:.2e}; up EPE mean {mu:.2e} max {xu:.2e}")
     assert ml <= 1e-4 and mu <= 1e-4, (ml, mu)
     assert xl <= 1e-3 and xu <= 1e-3, (xl, xu)
 
@@ -91,3 +93,50 @@ def test_fused_update_matches_module_update_block():
     for ref, got in zip((n1, m1, d1, n2, m2, d2), (*f1, *f2)):
         err = float((ref - got).abs().max())
         assert err <= 1e-4 * max(1.0, float(ref.abs().max())), err
+
+
+class _FixedCorr:
+    """Stands in for CorrBlock: hands the given lookup outputs to SplitUpdate (as S32) in order."""
+
+    def __init__(self, corrs):
+        self.corrs = list(corrs)
+
+    def lookup_s32(self, coords, out):
+        from optical_flow import _native
+
+        _native.pack_s32(self.corrs.pop(0), "none", _native.S32Slice(out))
+        return out
+
+
+def test_split_update_matches_module_update_block():
+    """SplitUpdate (split-fp16 convolutions, fused GRU / motion / flow-head epilogues, in-place coords) against the
+    nn.Module update block (MIOpen fp32) on the same GPU, two steps so the carried state is checked too."""
+    from model.update import SplitUpdate
+    from model.utils import coords_grid
+
+    model = _model(RAFT)
+    block = model.update_block
+    b, h, w = 2, 24, 40
+    g = lambda s, shape, std: torch.from_numpy(synthetic.hash_normal(s, shape, std)).to(DEV)
+    cnet_out = g(1, (b, 256, h, w), 1.0)
+    net, inp = torch.tanh(cnet_out[:, :128]), torch.relu(cnet_out[:, 128:])
+    corr1, corr2 = g(3, (b, 324, h, w), 2.0), g(4, (b, 324, h, w), 2.0)
+    coords0 = coords_grid(b, h, w, device=DEV)
+    coords1 = coords0 + g(5, (b, 2, h, w), 3.0)
+    with torch.inference_mode():
+        n1, m1, d1 = block(net, inp, corr1, coords1 - coords0)
+        c1 = coords1 + d1
+        n2, m2, d2 = block(n1, inp, corr2, c1 - coords0)
+        c2 = c1 + d2
+        runner = SplitUpdate(block, cnet_out.contiguous(), 128)
+        cc = coords1.clone()
+        fake = _FixedCorr([corr1, corr2])
+        s1 = runner.step(fake, cc, need_mask=True)
+        cc1 = cc.clone()
+        h1 = runner.hm.view(b, h, w, 128).permute(0, 3, 1, 2).clone()
+        s2 = runner.step(fake, cc, need_mask=True)
+        h2 = runner.hm.view(b, h, w, 128).permute(0, 3, 1, 2)
+    for what, ref, got in (("net1", n1, h1), ("mask1", m1, s1), ("coords1", c1, cc1), ("net2", n2, h2), ("mask2", m2, s2), ("coords2", c2, cc)):
+        err = float((ref - got).abs().max())
+        print(f"{what}: max |d| {err:.2e}")
+        assert err <= 1e-4 * max(1.0, float(ref.abs().max())), (what, err)

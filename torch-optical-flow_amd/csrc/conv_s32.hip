@@ -1,0 +1,405 @@
+// Split-fp16 implicit-GEMM convolution for the RAFT update block (gfx950).
+//
+// Replaces the nn.Conv2d layers of methods/raft/model/update.py:40-161 (BasicMotionEncoder, SepConvGRU,
+// FlowHead, mask head) at fp32 accuracy on the fp16 matrix cores.
+//
+// Numerics. Every operand is carried as an unevaluated sum of two fp16 values, x = hi + lo (hi = fp16(x),
+// lo = fp16(x - hi): 22 significant bits), and every product as three v_mfma_f32_32x32x16_f16:
+// hi*hi + hi*lo + lo*hi (the lo*lo term is below fp32 rounding), accumulated in fp32. Weights are scaled per
+// output channel by a power of two (max |w| -> 2^14, undone exactly in the epilogue) so that their lo parts stay
+// normal fp16. tools/exp/split_numerics.py measured RAFT at Sintel size with this arithmetic: 3.7e-6 px mean
+// EPE against the reference's fp32 CPU flow, the same as fp32 reordering noise.
+//
+// Activation format "S32" (include/oflow.h): NHWC by groups of 32 channels, one group of one pixel = one 128-B
+// line = hi[32] fp16 then lo[32] fp16. A channel slice of a wider S32 buffer is (base + g0 * 128, pixel stride).
+// Packed weights: [input groups][taps][n_pad][hi[32] | lo[32]] fp16 (the same line format, one line per output
+// channel and k32 chunk), so both MFMA operands stage as whole lines.
+//
+// Workgroup tile: 4 output rows x 32 output columns (128 pixels) x BN output channels; 4 waves as WM x WN.
+// Loop: input groups (k32) outer, taps inner. Per group the (4 + KH - 1) x (32 + KW - 1) input halo is staged in
+// LDS once and read by every tap at a shifted offset; per (group, tap) a BN x 128-B weight slab is staged (double
+// buffered). Both are register-staged one step ahead. LDS lines are 16-B-slot swizzled (slot ^= (row >> 1) & 7)
+// so that the 32 rows of an MFMA operand read by ds_read_b128 are bank-conflict free from any starting row.
+// Epilogue: accumulators -> LDS tile [pixel][channel] fp32 -> per-channel scale, bias, activation and the fused
+// consumer (S32 stores with 16-B chunks, GRU gates, fp32 NCHW store/accumulate).
+#include "oflow_internal.h"
+
+namespace oflow {
+namespace {
+
+typedef _Float16 half8 __attribute__((ext_vector_type(8)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));  // native vector: stays in VGPRs (HIP uint4 is copied by memcpy)
+
+constexpr int kTY = 4, kTX = 32, kBM = kTY * kTX, kThreads = 256;
+
+__device__ __forceinline__ int swz(int row) { return (row >> 1) & 7; }
+
+struct ConvArgs {
+  const uint8_t* x;        // S32 input, first group of the slice
+  long long xps;           // input pixel stride (bytes)
+  int kg;                  // input groups (k32 chunks)
+  const uint8_t* w;        // packed weights
+  int npad;                // padded output channels in the packing
+  const float* wsc;        // [npad] inverse weight scale
+  const float* bias;       // [N] or null
+  int N;                   // real output channels
+  int B, H, W, tiles_x, tiles_y;
+  int act;                 // 0 none, 1 relu, 2 sigmoid, 3 tanh
+  float oscale;            // applied after the activation
+  uint8_t* y0;             // S32 destination 0 (first group) or null
+  long long y0ps;
+  uint8_t* y1;             // S32 destination 1 or null
+  long long y1ps;
+  float* f;                // fp32 NCHW destination or null
+  long long fbs, fcs;      // its batch / channel strides (floats)
+  int faccum;              // 1: f += value
+  // GRU (EPI 1 = z|r gates, EPI 2 = candidate + blend); NHWC fp32 [P][gch]
+  float* h;
+  float* z;
+  int gch;
+};
+
+__device__ __forceinline__ float act_fn(float v, int act) {
+  if (act == 1) return v < 0.f ? 0.f : v;  // relu; NaN propagates like ATen
+  if (act == 2) return 1.0f / (1.0f + expf(-v));
+  if (act == 3) return tanhf(v);
+  return v;
+}
+
+__device__ __forceinline__ void split8(const float* v, half8& hi, half8& lo) {
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const _Float16 a = static_cast<_Float16>(v[j]);
+    hi[j] = a;
+    lo[j] = static_cast<_Float16>(v[j] - static_cast<float>(a));
+  }
+}
+
+// store channels [n, n + 8) of pixel P (n % 8 == 0) into an S32 destination, only those < N
+__device__ __forceinline__ void store_s32(uint8_t* y, long long ps, long long P, int n, int N, const float* v) {
+  uint8_t* line = y + P * ps + (long long)(n >> 5) * 128 + ((n & 31) >> 3) * 16;
+  if (n + 8 <= N) {
+    half8 hi, lo;
+    split8(v, hi, lo);
+    *reinterpret_cast<half8*>(line) = hi;
+    *reinterpret_cast<half8*>(line + 64) = lo;
+  } else {
+    _Float16* hp = reinterpret_cast<_Float16*>(line);
+    _Float16* lp = reinterpret_cast<_Float16*>(line + 64);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      if (n + j < N) {
+        const _Float16 a = static_cast<_Float16>(v[j]);
+        hp[j] = a;
+        lp[j] = static_cast<_Float16>(v[j] - static_cast<float>(a));
+      }
+    }
+  }
+}
+
+template <int KH, int KW, int BN, int WM, int WN, int EPI>
+__global__ __launch_bounds__(kThreads, 2) void conv_s32_kernel(ConvArgs a) {
+  constexpr int T = KH * KW;
+  constexpr int PH = KH / 2, PW = KW / 2;
+  constexpr int HY = kTY + KH - 1, HX = kTX + KW - 1, NPIX = HY * HX;
+  constexpr int AITEMS = NPIX * 8, APER = (AITEMS + kThreads - 1) / kThreads;
+  constexpr int BITEMS = BN * 8, BPER = (BITEMS + kThreads - 1) / kThreads;
+  constexpr int MT = kTY / WM;            // 32-pixel row tiles per wave
+  constexpr int NT = BN / WN / 32;        // 32-channel column tiles per wave
+  static_assert(WM * WN == 4 && MT >= 1 && NT >= 1, "bad wave grid");
+  constexpr int A_BYTES = NPIX * 128, B_BYTES = BN * 128;
+  constexpr int MAIN_BYTES = A_BYTES + 2 * B_BYTES;
+  constexpr int TS = BN + 4;              // epilogue tile row stride (floats)
+  constexpr int EPI_BYTES = kBM * TS * 4;
+  constexpr int LDS_BYTES = MAIN_BYTES > EPI_BYTES ? MAIN_BYTES : EPI_BYTES;
+  __shared__ __attribute__((aligned(16))) uint8_t smem[LDS_BYTES];
+  uint8_t* sA = smem;
+  uint8_t* sB = smem + A_BYTES;
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave / WN, wn = wave % WN;
+  const int r = lane & 31, hh = lane >> 5;
+
+  int tile = blockIdx.x;
+  const int tx0 = (tile % a.tiles_x) * kTX;
+  tile /= a.tiles_x;
+  const int ty0 = (tile % a.tiles_y) * kTY;
+  const int b = tile / a.tiles_y;
+  const int n0 = blockIdx.y * BN;
+  const long long pix0 = (long long)b * a.H * a.W;
+
+  u32x4 ra[APER], rb[BPER];
+  // staging item -> (halo pixel p, 16-B chunk c): source offset (-1: outside the image -> zeros)
+#define OFLOW_LOAD_A(G)                                                                                              \
+  _Pragma("unroll") for (int s_ = 0; s_ < APER; ++s_) {                                                              \
+    const int item = tid + s_ * kThreads;                                                                            \
+    const int p = item >> 3, c = item & 7;                                                                           \
+    const int gy = ty0 - PH + p / HX, gx = tx0 - PW + p % HX;                                                        \
+    const bool ok = (AITEMS % kThreads == 0 || item < AITEMS) && static_cast<unsigned>(gy) < static_cast<unsigned>(a.H) && \
+                    static_cast<unsigned>(gx) < static_cast<unsigned>(a.W);                                          \
+    ra[s_] = ok ? *reinterpret_cast<const u32x4*>(a.x + (pix0 + (long long)gy * a.W + gx) * a.xps + (G) * 128 + c * 16) \
+                : u32x4{0u, 0u, 0u, 0u};                                                                             \
+  }
+#define OFLOW_WRITE_A()                                                                                              \
+  _Pragma("unroll") for (int s_ = 0; s_ < APER; ++s_) {                                                              \
+    const int item = tid + s_ * kThreads;                                                                            \
+    const int p = item >> 3, c = item & 7;                                                                           \
+    if (AITEMS % kThreads == 0 || item < AITEMS) *reinterpret_cast<u32x4*>(sA + p * 128 + ((c ^ swz(p)) << 4)) = ra[s_]; \
+  }
+#define OFLOW_LOAD_B(STEP)                                                                                           \
+  _Pragma("unroll") for (int s_ = 0; s_ < BPER; ++s_) {                                                              \
+    const int item = tid + s_ * kThreads;                                                                            \
+    if (BITEMS % kThreads == 0 || item < BITEMS)                                                                     \
+      rb[s_] = *reinterpret_cast<const u32x4*>(a.w + ((long long)(STEP) * a.npad + n0) * 128 + item * 16);           \
+  }
+#define OFLOW_WRITE_B(BUF)                                                                                           \
+  _Pragma("unroll") for (int s_ = 0; s_ < BPER; ++s_) {                                                              \
+    const int item = tid + s_ * kThreads;                                                                            \
+    const int n = item >> 3, c = item & 7;                                                                           \
+    if (BITEMS % kThreads == 0 || item < BITEMS)                                                                     \
+      *reinterpret_cast<u32x4*>(sB + (BUF) * B_BYTES + n * 128 + ((c ^ swz(n)) << 4)) = rb[s_];                      \
+  }
+
+  f32x16 acc[MT][NT];
+#pragma unroll
+  for (int i = 0; i < MT; ++i)
+#pragma unroll
+    for (int j = 0; j < NT; ++j)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
+
+  const int S = a.kg * T;
+  OFLOW_LOAD_A(0);
+  OFLOW_LOAD_B(0);
+  OFLOW_WRITE_A();
+  OFLOW_WRITE_B(0);
+  __syncthreads();
+
+  for (int i = 0; i < S; ++i) {
+    const int g = i / T, t = i - g * T;
+    const bool nextB = i + 1 < S;
+    const bool nextA = (t == T - 1) && (g + 1 < a.kg);
+    if (nextB) { OFLOW_LOAD_B(i + 1); }
+    if (nextA) { OFLOW_LOAD_A(g + 1); }
+
+    const int ky = t / KW, kx = t - ky * KW;
+    const uint8_t* bufB = sB + (i & 1) * B_BYTES;
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      half8 ahi[MT], alo[MT], bhi[NT], blo[NT];
+      const int chi = 2 * s + hh, clo = 4 + 2 * s + hh;
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) {
+        const int p = (wm * MT + mt + ky) * HX + r + kx;
+        const uint8_t* row = sA + p * 128;
+        ahi[mt] = *reinterpret_cast<const half8*>(row + ((chi ^ swz(p)) << 4));
+        alo[mt] = *reinterpret_cast<const half8*>(row + ((clo ^ swz(p)) << 4));
+      }
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt) {
+        const int n = wn * (BN / WN) + nt * 32 + r;
+        const uint8_t* row = bufB + n * 128;
+        bhi[nt] = *reinterpret_cast<const half8*>(row + ((chi ^ swz(n)) << 4));
+        blo[nt] = *reinterpret_cast<const half8*>(row + ((clo ^ swz(n)) << 4));
+      }
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt) {
+          acc[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ahi[mt], blo[nt], acc[mt][nt], 0, 0, 0);
+          acc[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(alo[mt], bhi[nt], acc[mt][nt], 0, 0, 0);
+          acc[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ahi[mt], bhi[nt], acc[mt][nt], 0, 0, 0);
+        }
+    }
+
+    if (nextA) {
+      __syncthreads();  // every wave is done with A(g)
+      OFLOW_WRITE_A();
+    }
+    if (nextB) { OFLOW_WRITE_B((i + 1) & 1); }
+    __syncthreads();
+  }
+
+#undef OFLOW_LOAD_A
+#undef OFLOW_WRITE_A
+#undef OFLOW_LOAD_B
+#undef OFLOW_WRITE_B
+
+  // ---- epilogue: accumulators -> LDS tile [pixel][channel] ----
+  float* sT = reinterpret_cast<float*>(smem);
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt) {
+      const int nl = wn * (BN / WN) + nt * 32 + r;
+      const int pbase = (wm * MT + mt) * kTX;
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        const int m = (e & 3) + 8 * (e >> 2) + 4 * hh;
+        sT[(pbase + m) * TS + nl] = acc[mt][nt][e];
+      }
+    }
+  __syncthreads();
+
+  if (a.f != nullptr) {
+    // fp32 NCHW: lanes = consecutive pixels of one tile row (128-B rows of the destination)
+    for (int item = tid; item < kBM * BN; item += kThreads) {
+      const int nl = item / kBM, pl = item - nl * kBM;
+      const int n = n0 + nl;
+      const int y = ty0 + pl / kTX, x = tx0 + (pl % kTX);
+      if (n < a.N && y < a.H && x < a.W) {
+        float v = sT[pl * TS + nl] * a.wsc[n];
+        if (a.bias) v += a.bias[n];
+        v = act_fn(v, a.act) * a.oscale;
+        float* d = a.f + b * a.fbs + n * a.fcs + (long long)y * a.W + x;
+        if (a.faccum)
+          *d = *d + v;
+        else
+          *d = v;
+      }
+    }
+  }
+  if (a.y0 == nullptr && EPI == 0) return;
+
+  // S32 / GRU consumers: one thread = one pixel x 8 consecutive channels
+  constexpr int C8 = BN / 8;
+  for (int item = tid; item < kBM * C8; item += kThreads) {
+    const int pl = item / C8, c8 = item - pl * C8;
+    const int nl = c8 * 8, n = n0 + nl;
+    const int y = ty0 + pl / kTX, x = tx0 + (pl % kTX);
+    if (n >= a.N || y >= a.H || x >= a.W) continue;
+    const long long P = pix0 + (long long)y * a.W + x;
+    const float4 t0 = *reinterpret_cast<const float4*>(&sT[pl * TS + nl]);
+    const float4 t1 = *reinterpret_cast<const float4*>(&sT[pl * TS + nl + 4]);
+    float v[8] = {t0.x, t0.y, t0.z, t0.w, t1.x, t1.y, t1.z, t1.w};
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int nj = n + j < a.N ? n + j : a.N - 1;
+      v[j] = v[j] * a.wsc[nj] + (a.bias ? a.bias[nj] : 0.f);
+    }
+    if constexpr (EPI == 0) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = act_fn(v[j], a.act) * a.oscale;
+      store_s32(a.y0, a.y0ps, P, n, a.N, v);
+      if (a.y1) store_s32(a.y1, a.y1ps, P, n, a.N, v);
+    } else if constexpr (EPI == 1) {
+      // [z | r] gates (update.py:91-96): z = sigmoid -> a.z; r*h = sigmoid(r) * h -> S32 y0 (channel n - gch)
+      if (n < a.gch) {
+        float* zp = a.z + P * a.gch + n;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) zp[j] = 1.0f / (1.0f + expf(-v[j]));
+      } else {
+        const float* hp = a.h + P * a.gch + (n - a.gch);
+        float rh[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) rh[j] = (1.0f / (1.0f + expf(-v[j]))) * hp[j];
+        store_s32(a.y0, a.y0ps, P, n - a.gch, a.gch, rh);
+      }
+    } else {
+      // candidate + blend (update.py:96-97): h = (1 - z) * h + z * tanh(q); h (fp32) in place + S32 y0
+      float* hp = a.h + P * a.gch + n;
+      const float* zp = a.z + P * a.gch + n;
+      float hn[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float q = tanhf(v[j]);
+        const float z = zp[j];
+        hn[j] = (1.0f - z) * hp[j] + z * q;
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) hp[j] = hn[j];
+      store_s32(a.y0, a.y0ps, P, n, a.N, hn);
+    }
+  }
+}
+
+template <int KH, int KW, int BN, int WM, int WN, int EPI>
+int launch_conv(const ConvArgs& a, hipStream_t s) {
+  dim3 grid(a.tiles_x * a.tiles_y * a.B, a.npad / BN);
+  hipLaunchKernelGGL((conv_s32_kernel<KH, KW, BN, WM, WN, EPI>), grid, dim3(kThreads), 0, s, a);
+  return launch_status();
+}
+
+template <int KH, int KW, int EPI>
+int launch_bn(const ConvArgs& a, int bn, hipStream_t s) {
+  switch (bn) {
+    case 128: return launch_conv<KH, KW, 128, 2, 2, EPI>(a, s);
+    case 64: return launch_conv<KH, KW, 64, 2, 2, EPI>(a, s);
+    case 32: return launch_conv<KH, KW, 32, 4, 1, EPI>(a, s);
+    default: return OFLOW_E_SHAPE;
+  }
+}
+
+}  // namespace
+}  // namespace oflow
+
+using namespace oflow;
+
+extern "C" int oflow_conv_s32(const void* d_x, long long x_pixel_stride, int in_groups, const void* d_wpack, int n_pad,
+                              const float* d_wscale, const float* d_bias, int N, int B, int H, int W, int kh, int kw,
+                              int block_n, int epilogue, int activation, float out_scale, void* d_y0,
+                              long long y0_pixel_stride, void* d_y1, long long y1_pixel_stride, float* d_f32,
+                              long long f32_batch_stride, long long f32_channel_stride, int f32_accumulate,
+                              float* d_gru_h, float* d_gru_z, int gru_channels, void* stream) {
+  if (!d_x || !d_wpack || !d_wscale) return OFLOW_E_NULL;
+  if (B <= 0 || H <= 0 || W <= 0 || N <= 0 || in_groups <= 0 || n_pad < N || n_pad % block_n) return OFLOW_E_SHAPE;
+  if (activation < 0 || activation > 3 || epilogue < 0 || epilogue > 2) return OFLOW_E_MODE;
+  if ((x_pixel_stride & 127) || ((uintptr_t)d_x & 15) || ((uintptr_t)d_wpack & 15)) return OFLOW_E_ALIGN;
+  if (epilogue == 0 && !d_y0 && !d_f32) return OFLOW_E_NULL;
+  if (epilogue != 0 && (!d_y0 || !d_gru_h || !d_gru_z || gru_channels <= 0 || gru_channels % 8)) return OFLOW_E_NULL;
+  if (epilogue == 1 && N != 2 * gru_channels) return OFLOW_E_SHAPE;
+  if (epilogue == 2 && N != gru_channels) return OFLOW_E_SHAPE;
+  if ((d_y0 && ((y0_pixel_stride & 127) || ((uintptr_t)d_y0 & 15))) ||
+      (d_y1 && ((y1_pixel_stride & 127) || ((uintptr_t)d_y1 & 15))))
+    return OFLOW_E_ALIGN;
+  ConvArgs a{};
+  a.x = static_cast<const uint8_t*>(d_x);
+  a.xps = x_pixel_stride;
+  a.kg = in_groups;
+  a.w = static_cast<const uint8_t*>(d_wpack);
+  a.npad = n_pad;
+  a.wsc = d_wscale;
+  a.bias = d_bias;
+  a.N = N;
+  a.B = B;
+  a.H = H;
+  a.W = W;
+  a.tiles_x = (W + kTX - 1) / kTX;
+  a.tiles_y = (H + kTY - 1) / kTY;
+  a.act = activation;
+  a.oscale = out_scale;
+  a.y0 = static_cast<uint8_t*>(d_y0);
+  a.y0ps = y0_pixel_stride;
+  a.y1 = static_cast<uint8_t*>(d_y1);
+  a.y1ps = y1_pixel_stride;
+  a.f = d_f32;
+  a.fbs = f32_batch_stride;
+  a.fcs = f32_channel_stride;
+  a.faccum = f32_accumulate;
+  a.h = d_gru_h;
+  a.z = d_gru_z;
+  a.gch = gru_channels;
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  const int key = kh * 16 + kw;
+  switch (epilogue) {
+    case 0:
+      switch (key) {
+        case 0x11: return launch_bn<1, 1, 0>(a, block_n, s);
+        case 0x33: return launch_bn<3, 3, 0>(a, block_n, s);
+        case 0x15: return launch_bn<1, 5, 0>(a, block_n, s);
+        case 0x51: return launch_bn<5, 1, 0>(a, block_n, s);
+        default: return OFLOW_E_SHAPE;
+      }
+    case 1:
+      if (block_n != 128) return OFLOW_E_SHAPE;
+      if (key == 0x15) return launch_conv<1, 5, 128, 2, 2, 1>(a, s);
+      if (key == 0x51) return launch_conv<5, 1, 128, 2, 2, 1>(a, s);
+      return OFLOW_E_SHAPE;
+    default:
+      if (block_n != 128) return OFLOW_E_SHAPE;
+      if (key == 0x15) return launch_conv<1, 5, 128, 2, 2, 2>(a, s);
+      if (key == 0x51) return launch_conv<5, 1, 128, 2, 2, 2>(a, s);
+      return OFLOW_E_SHAPE;
+  }
+}

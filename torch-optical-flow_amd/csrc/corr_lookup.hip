@@ -140,6 +140,111 @@ __global__ __launch_bounds__(kThreads) void corr_lookup_kernel(LookupArgs a) {
   }
 }
 
+// S32 variant (split-fp16 NHWC, conv_s32.hip) feeding the update block's convc1 directly: one workgroup = 64 queries
+// x ALL levels (looped), so the 4 level segments of a pixel's 1408-B output row are written by one workgroup
+// within a few microseconds; lanes walk the channels of one query (2-B hi / lo stores, contiguous runs).
+// Channels L*(2r+1)^2 .. 32*G-1 of the destination are padding and are never written (zeroed once by the host).
+template <int R>
+__global__ __launch_bounds__(kThreads) void corr_lookup_s32_kernel(LookupArgs a, int nlev, uint8_t* out, long long ops) {
+  constexpr int PK = 2 * R + 2;
+  constexpr int K = 2 * R + 1;
+  constexpr int KK = K * K;
+  constexpr int PS = PK * PK;
+  constexpr int QS = PS + 1;
+  constexpr int ITEMS = kQ * PS;
+  constexpr int PER = (ITEMS + kThreads - 1) / kThreads;
+  constexpr int OUTS = kQ * KK;
+  constexpr int PERO = (OUTS + kThreads - 1) / kThreads;
+
+  __shared__ float sP[kQ * QS];
+  __shared__ int sX[kQ], sY[kQ];
+  __shared__ float4 sW[kQ];
+  __shared__ float sC[kQ][2];
+
+  const int q0 = blockIdx.x * kQ;
+  if (threadIdx.x < kQ) {
+    const int q = q0 + threadIdx.x;
+    float cx = 0.f, cy = 0.f;
+    if (q < a.total) {
+      const int b = q / a.N;
+      const int pix = q - b * a.N;
+      cx = a.coords[(size_t)(2 * b) * a.N + pix];
+      cy = a.coords[(size_t)(2 * b + 1) * a.N + pix];
+    }
+    sC[threadIdx.x][0] = cx;
+    sC[threadIdx.x][1] = cy;
+  }
+  for (int lvl = 0; lvl < nlev; ++lvl) {
+    const int Hl = a.Hl[lvl], Wl = a.Wl[lvl];
+    const int HB = a.HB[lvl], WB = a.WB[lvl];
+    const float* __restrict__ L = a.lv[lvl];
+    const float inv = 1.0f / static_cast<float>(1 << lvl);
+    __syncthreads();  // sC written / previous level's patches consumed
+    if (threadIdx.x < kQ) {
+      const float cx = sC[threadIdx.x][0] * inv, cy = sC[threadIdx.x][1] * inv;
+      int xs = -(1 << 28), ys = -(1 << 28);
+      float4 w = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (fabsf(cx) < 4194304.0f && fabsf(cy) < 4194304.0f) {
+        const float fx = floorf(cx), fy = floorf(cy);
+        const float wx = cx - fx, wy = cy - fy;
+        const float ex = 1.0f - wx, ey = 1.0f - wy;
+        xs = static_cast<int>(fx) - R;
+        ys = static_cast<int>(fy) - R;
+        w = make_float4(ey * ex, ey * wx, wy * ex, wy * wx);
+      }
+      sX[threadIdx.x] = xs;
+      sY[threadIdx.x] = ys;
+      sW[threadIdx.x] = w;
+    }
+    __syncthreads();
+    float v[PER];
+#pragma unroll
+    for (int s = 0; s < PER; ++s) {
+      const int item = threadIdx.x + kThreads * s;
+      v[s] = 0.0f;
+      if (item < ITEMS) {
+        const int q = item / PS;
+        const int rem = item - q * PS;
+        const int row = rem / PK;
+        const int col = rem - row * PK;
+        const int y = sY[q] + row, x = sX[q] + col;
+        if (q0 + q < a.total && static_cast<unsigned>(y) < static_cast<unsigned>(Hl) &&
+            static_cast<unsigned>(x) < static_cast<unsigned>(Wl))
+          v[s] = L[(((size_t)(q0 + q) * HB + (y >> 2)) * WB + (x >> 3)) * 32 + ((y & 3) << 3) + (x & 7)];
+      }
+    }
+#pragma unroll
+    for (int s = 0; s < PER; ++s) {
+      const int item = threadIdx.x + kThreads * s;
+      if (item < ITEMS) {
+        const int q = item / PS;
+        sP[q * QS + (item - q * PS)] = v[s];
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int s = 0; s < PERO; ++s) {
+      const int o = threadIdx.x + kThreads * s;
+      if (o < OUTS) {
+        const int q = o / KK;
+        const int k = o - q * KK;
+        if (q0 + q < a.total) {
+          const int i = k / K;  // moves x (Q1)
+          const int j = k - i * K;
+          const float* p = &sP[q * QS + j * PK + i];
+          const float4 w = sW[q];
+          const float val = p[0] * w.x + p[1] * w.y + p[PK] * w.z + p[PK + 1] * w.w;
+          const int c = lvl * KK + k;
+          _Float16* line = reinterpret_cast<_Float16*>(out + (long long)(q0 + q) * ops + (c >> 5) * 128) + (c & 31);
+          const _Float16 hi = static_cast<_Float16>(val);
+          line[0] = hi;
+          line[32] = static_cast<_Float16>(val - static_cast<float>(hi));
+        }
+      }
+    }
+  }
+}
+
 template <int R>
 int launch_lookup(const LookupArgs& a, int nlev, hipStream_t s, bool tiled) {
   dim3 grid((a.total + kQ - 1) / kQ, nlev);
@@ -204,4 +309,42 @@ extern "C" int oflow_corr_lookup_tiled_f32(const float* const* d_levels, const i
                                            int num_levels, const float* d_coords, int B, int H, int W, int radius,
                                            float* d_out, void* stream) {
   return corr_lookup_impl(d_levels, level_h, level_w, num_levels, d_coords, B, H, W, radius, d_out, stream, true);
+}
+
+extern "C" int oflow_corr_lookup_tiled_s32(const float* const* d_levels, const int* level_h, const int* level_w,
+                                           int num_levels, const float* d_coords, int B, int H, int W, int radius,
+                                           void* d_out, long long out_pixel_stride, void* stream) {
+  if (!d_levels || !level_h || !level_w || !d_coords || !d_out) return OFLOW_E_NULL;
+  if (B <= 0 || H <= 0 || W <= 0) return OFLOW_E_SHAPE;
+  if (num_levels < 1 || num_levels > OFLOW_MAX_LEVELS) return OFLOW_E_LEVELS;
+  if (radius < 0 || radius > OFLOW_MAX_RADIUS) return OFLOW_E_RADIUS;
+  if ((long long)B * H * W >= (1ll << 31) / 64) return OFLOW_E_SHAPE;
+  const int K = 2 * radius + 1;
+  if (out_pixel_stride < (long long)((num_levels * K * K + 31) / 32) * 128) return OFLOW_E_SHAPE;
+  if ((out_pixel_stride & 127) || ((uintptr_t)d_out & 15)) return OFLOW_E_ALIGN;
+  LookupArgs a{};
+  for (int l = 0; l < num_levels; ++l) {
+    if (!d_levels[l]) return OFLOW_E_NULL;
+    if (level_h[l] < 2 || level_w[l] < 2) return OFLOW_E_TINY;
+    a.lv[l] = d_levels[l];
+    a.Hl[l] = level_h[l];
+    a.Wl[l] = level_w[l];
+    a.HB[l] = (level_h[l] + 3) / 4;
+    a.WB[l] = (level_w[l] + 7) / 8;
+  }
+  a.coords = d_coords;
+  a.N = H * W;
+  a.total = B * H * W;
+  a.cout = num_levels * K * K;
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  dim3 grid((a.total + kQ - 1) / kQ);
+  uint8_t* out = static_cast<uint8_t*>(d_out);
+  switch (radius) {
+#define OFLOW_CASE(RR) \
+  case RR: hipLaunchKernelGGL((corr_lookup_s32_kernel<RR>), grid, dim3(kThreads), 0, s, a, num_levels, out, out_pixel_stride); break;
+    OFLOW_CASE(0) OFLOW_CASE(1) OFLOW_CASE(2) OFLOW_CASE(3) OFLOW_CASE(4) OFLOW_CASE(5) OFLOW_CASE(6) OFLOW_CASE(7)
+#undef OFLOW_CASE
+    default: return OFLOW_E_RADIUS;
+  }
+  return launch_status();
 }

@@ -47,6 +47,15 @@ class CorrBlock:
             return _native.corr_lookup_tiled(self._tiled, coords, self.radius)
         return _native.corr_lookup(self._pyramid, coords, self.radius)
 
+    def lookup_s32(self, coords: Tensor, out: Tensor) -> Tensor:
+        """The lookup written as split-fp16 NHWC (S32) into ``out`` for the update block's convc1 (an addition;
+        values equal ``__call__``'s up to the fp16 hi/lo representation of 22 significant bits)."""
+        if self._tiled is not None:
+            return _native.corr_lookup_tiled_s32(self._tiled, coords, self.radius, out)
+        corr = _native.corr_lookup(self._pyramid, coords, self.radius)
+        _native.pack_s32(corr, "none", _native.S32Slice(out))
+        return out
+
     @staticmethod
     def corr(fmap1: Tensor, fmap2: Tensor) -> Tensor:
         """All-pairs volume (B, H, W, 1, H, W) / sqrt(C) (`corr.py:79-87`)."""
@@ -70,3 +79,8 @@ class AlternateCorrBlock:
 
     def __call__(self, coords: Tensor) -> Tensor:
         return _native.corr_lookup_otf(self.fmap1_f16, self.fmap2_pyramid_f16, coords, self.radius)
+
+    def lookup_s32(self, coords: Tensor, out: Tensor) -> Tensor:
+        """``__call__`` repacked as split-fp16 NHWC (S32) into ``out`` for the update block."""
+        _native.pack_s32(self(coords), "none", _native.S32Slice(out))
+        return out

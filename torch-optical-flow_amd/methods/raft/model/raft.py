@@ -10,9 +10,11 @@ values; three output-identical changes remove host work from the loop:
   * coordinate grids are built on the device (no CPU build + H2D copy, `raft.py:68-69`);
   * with ``test_mode=True`` only the last iteration's convex upsampling is computed — the reference computes
     all ``iters`` and returns only the last (Q11, `raft.py:136-145`);
-  * without autograd on the GPU the update block runs through ``FusedUpdate`` (fused bias/activation/GRU
-    elementwise kernels over persistent concatenated buffers; same weights and arithmetic up to rounding), and in
-    test mode its mask head (two convolutions feeding only the upsampling) runs at the last iteration only.
+  * without autograd on the GPU the update block runs through ``SplitUpdate``: every convolution on the
+    split-fp16 matrix-core kernel (fp32-level accuracy) with the GRU gates, activations, concatenations and the
+    ``coords1 += delta_flow`` update fused into convolution epilogues (``update_impl = "fused"`` selects the
+    MIOpen-based ``FusedUpdate`` instead); in test mode the mask head (two convolutions feeding only the
+    upsampling) runs at the last iteration only.
 """
 from __future__ import annotations
 
@@ -26,7 +28,7 @@ from torch import Tensor
 
 from .corr import AlternateCorrBlock, CorrBlock
 from .extractor import BasicEncoder
-from .update import BasicUpdateBlock, FusedUpdate
+from .update import BasicUpdateBlock, FusedUpdate, SplitUpdate
 from .utils import coords_grid, upflow8
 
 
@@ -79,7 +81,11 @@ class RAFT(nn.Module):
         self.fnet = BasicEncoder(output_dim=256, norm_fn="instance", dropout=dropout)
         self.cnet = BasicEncoder(output_dim=hidden_dim + context_dim, norm_fn="batch", dropout=dropout)
         self.update_block = BasicUpdateBlock(corr_levels=corr_levels, corr_radius=corr_radius, hidden_dim=hidden_dim)
-        self.fused_update = True  # plain attribute (not an hparam): False runs the nn.Module update block
+        # plain attributes (not hparams): how GPU inference runs the update block. "split": split-fp16 matrix-core
+        # convolutions with fused epilogues (SplitUpdate, default); "fused": MIOpen fp32 convolutions + fused
+        # elementwise kernels (FusedUpdate); "module": the nn.Module as written. fused_update=False forces "module".
+        self.update_impl = "split"
+        self.fused_update = True
 
     # -- checkpoints -------------------------------------------------------------------------------------
     @classmethod
@@ -141,20 +147,34 @@ class RAFT(nn.Module):
         block = AlternateCorrBlock if self.hparams.get("alternate_corr", False) else CorrBlock
         corr_fn = block(fmap1.float(), fmap2.float(), radius=self.hparams.corr_radius)
 
-        net, inp = torch.split(self.cnet(image0), [hdim, cdim], dim=1)
-        net = torch.tanh(net)
-        inp = torch.relu(inp)
-
+        cnet_out = self.cnet(image0)
         coords0, coords1 = self.initialize_flow(image0)
         if flow_init is not None:
             coords1 = coords1 + flow_init
 
-        # inference on the GPU: fused update block (same weights and math, persistent [h | x] buffers)
-        fused = net.is_cuda and not torch.is_grad_enabled() and self.fused_update
-        runner = FusedUpdate(self.update_block, net, inp) if fused else None
-
+        gpu_inference = cnet_out.is_cuda and not torch.is_grad_enabled() and self.fused_update
+        impl = self.update_impl if gpu_inference else "module"
         flow_predictions = []
         flow_up = None
+        if impl == "split":
+            # coords1 is advanced in place by the flow head's epilogue (raft.py:133)
+            runner = SplitUpdate(self.update_block, cnet_out, hdim)
+            coords1 = coords1.contiguous()
+            for itr in range(iters):
+                last = itr == iters - 1
+                up_mask = runner.step(corr_fn, coords1, need_mask=not test_mode or last)
+                if test_mode and not last:
+                    continue  # Q11: intermediate upsamplings are never returned in test mode
+                flow_up = self.upsample_flow(coords1 - coords0, up_mask)
+                flow_predictions.append(flow_up)
+            if test_mode:
+                return coords1 - coords0, flow_up
+            return flow_predictions
+
+        net, inp = torch.split(cnet_out, [hdim, cdim], dim=1)
+        net = torch.tanh(net)
+        inp = torch.relu(inp)
+        runner = FusedUpdate(self.update_block, net, inp) if impl == "fused" else None
         for itr in range(iters):
             coords1 = coords1.detach()
             corr = corr_fn(coords1)

@@ -155,3 +155,100 @@ class FusedUpdate:
             m = _native.bias_act_(self._conv(net, blk.mask[0]), blk.mask[0].bias, "relu")
             mask = _native.bias_act_(self._conv(m, blk.mask[2]), blk.mask[2].bias, "none", scale=0.25)
         return net, mask, delta_flow
+
+
+def _weights_key(block: nn.Module):
+    return tuple((q.data_ptr(), q._version) for q in block.parameters())
+
+
+class SplitUpdate:
+    """Inference execution of ``BasicUpdateBlock`` with every convolution on the split-fp16 matrix-core kernel
+    (``oflow_conv_s32``: operands as fp16 hi + lo pairs, three MFMAs per product, fp32 accumulation — fp32-level
+    accuracy, see csrc/conv_s32.hip) and every elementwise stage fused into a convolution epilogue.
+
+    Activations live in S32 buffers (split-fp16 NHWC by 32-channel groups, include/oflow.h), laid out so that no
+    concatenation is ever copied (`update.py:93, 96, 100, 103, 127, 155`):
+      hx  = [h | inp | motion(126) | flow(2)]   (GRU input of the z, r gates)     12 groups
+      rhx = [r*h | inp | motion | flow]          (GRU input of the candidate)      12 groups
+      cf  = [relu(convc2) (192) | relu(convf2) (64)]  (input of the motion conv)  8 groups
+    h is also kept in fp32 ([P, 128]) so that the blend h = (1-z)h + zq (`update.py:97`) runs in fp32.
+    Per iteration: lookup -> corr (S32), flow_prep -> flow channels + convf1's 7x7 patch matrix, then
+    convc1, convc2, convf1 (1x1 over the patches), convf2, conv (-> hx, rhx), [z|r] (-> z, r*h -> rhx),
+    q (-> h, hx) for the 1x5 and the 5x1 half, flow head conv1, conv2 (coords1 += delta in its epilogue), and at the
+    last iteration the mask head (1x1 conv 256 -> 576 with the x0.25 in its epilogue, fp32 NCHW).
+    """
+
+    def __init__(self, block: BasicUpdateBlock, cnet_out: Tensor, hdim: int) -> None:
+        b, c, h, w = cnet_out.shape
+        enc, gru = block.encoder, block.gru
+        cdim = c - hdim
+        if (hdim, cdim, enc.conv.out_channels, gru.convz1.in_channels) != (128, 128, 126, 384):
+            raise RuntimeError("SplitUpdate: supports the RAFT (large) update block only")
+        dev = cnet_out.device
+        self.block, self.shape = block, (b, h, w)
+        S = _native.s32_empty
+        self.hx = S(b, h, w, 12, dev)
+        self.rhx = S(b, h, w, 12, dev)
+        self.corr = S(b, h, w, (enc.convc1.in_channels + 31) // 32, dev, zero=True)
+        self.c1 = S(b, h, w, 8, dev)
+        self.cf = S(b, h, w, 8, dev)
+        self.pm = S(b, h, w, 4, dev)
+        self.f1 = S(b, h, w, 4, dev)
+        self.fh = S(b, h, w, 8, dev)
+        self.hm = torch.empty((b * h * w, hdim), device=dev, dtype=torch.float32)
+        self.z = torch.empty_like(self.hm)
+        V = _native.S32Slice
+        _native.pack_s32(cnet_out[:, :hdim], "tanh", V(self.hx, 0, 4), nhwc=self.hm)  # raft.py:117
+        _native.pack_s32(cnet_out[:, hdim:], "relu", V(self.hx, 4, 4), V(self.rhx, 4, 4))  # raft.py:118
+        self.w = self._weights(block)
+
+    @staticmethod
+    def _weights(block: BasicUpdateBlock):
+        key = _weights_key(block)
+        cache = block.__dict__.get("_split_weights")
+        if cache is not None and cache[0] == key:
+            return cache[1]
+        enc, gru, fh = block.encoder, block.gru, block.flow_head
+        CW = _native.ConvWeights
+        w = {
+            "c1": CW(enc.convc1.weight, enc.convc1.bias, 256),
+            "c2": CW(enc.convc2.weight, enc.convc2.bias, 192),
+            "f1": CW(enc.convf1.weight, enc.convf1.bias, 128, patches7=True),
+            "f2": CW(enc.convf2.weight, enc.convf2.bias, 64),
+            "mo": CW(enc.conv.weight, enc.conv.bias, 128),
+            "fh1": CW(fh.conv1.weight, fh.conv1.bias, 256),
+            "fh2": CW(fh.conv2.weight, fh.conv2.bias, 32),
+            "m1": CW(block.mask[0].weight, block.mask[0].bias, 256),
+            "m2": CW(block.mask[2].weight, block.mask[2].bias, 576),
+        }
+        for tag in ("1", "2"):
+            cz, cr, cq = (getattr(gru, f"conv{g}{tag}") for g in "zrq")
+            w["zr" + tag] = CW(torch.cat([cz.weight, cr.weight]), torch.cat([cz.bias, cr.bias]), 256)
+            w["q" + tag] = CW(cq.weight, cq.bias, 128)
+        block.__dict__["_split_weights"] = (key, w)
+        return w
+
+    def step(self, corr_fn, coords1: Tensor, need_mask: bool) -> Optional[Tensor]:
+        """One update (`update.py:150-161` + `raft.py:128-133`): coords1 is advanced IN PLACE by delta_flow.
+        Returns 0.25 * mask (B, 576, H, W) fp32 when ``need_mask``, else None."""
+        V, conv, w = _native.S32Slice, _native.conv_s32, self.w
+        corr_fn.lookup_s32(coords1, self.corr)
+        _native.flow_prep(coords1, self.pm, (V(self.hx), 382), (V(self.rhx), 382))
+        conv(V(self.corr), w["c1"], 128, "relu", y0=V(self.c1))
+        conv(V(self.c1), w["c2"], 64, "relu", y0=V(self.cf, 0, 6))
+        conv(V(self.pm), w["f1"], 128, "relu", y0=V(self.f1))
+        conv(V(self.f1), w["f2"], 64, "relu", y0=V(self.cf, 6, 2))
+        conv(V(self.cf), w["mo"], 128, "relu", y0=V(self.hx, 8, 4), y1=V(self.rhx, 8, 4))
+        for tag in ("1", "2"):
+            conv(V(self.hx), w["zr" + tag], 128, epilogue=1, y0=V(self.rhx, 0, 4), gru_h=self.hm, gru_z=self.z)
+            conv(V(self.rhx), w["q" + tag], 128, epilogue=2, y0=V(self.hx, 0, 4), gru_h=self.hm, gru_z=self.z)
+        net = V(self.hx, 0, 4)
+        conv(net, w["fh1"], 128, "relu", y0=V(self.fh))
+        conv(V(self.fh), w["fh2"], 32, f32=coords1, f32_accumulate=True)
+        if not need_mask:
+            return None
+        b, h, wd = self.shape
+        mask = torch.empty((b, 576, h, wd), device=coords1.device, dtype=torch.float32)
+        conv(net, w["m1"], 128, "relu", y0=V(self.fh))
+        conv(V(self.fh), w["m2"], 64, out_scale=0.25, f32=mask)
+        return mask

@@ -44,6 +44,10 @@ SYMBOLS = (
     "oflow_bias_act_f32",
     "oflow_gru_reset_f32",
     "oflow_gru_blend_f32",
+    "oflow_conv_s32",
+    "oflow_pack_s32_f32",
+    "oflow_flow_prep_s32",
+    "oflow_corr_lookup_tiled_s32",
 )
 
 _lib = None
@@ -57,12 +61,17 @@ def set_event_recorder(recorder):
     _recorder = recorder
 
 
+# ops whose launches are bracketed by events when a recorder is set (others only if the recorder has "*": True)
+_TIMED_DEFAULT = ("corr_lookup", "corr_pyramid", "corr_lookup_otf", "corr_otf_prepare", "grid_warp")
+
+
 class _Timed:
     __slots__ = ("what", "stream", "ev0")
 
     def __init__(self, what: str, device: torch.device):
         self.what = what
-        self.stream = torch.cuda.current_stream(device) if _recorder is not None else None
+        on = _recorder is not None and (what in _TIMED_DEFAULT or _recorder.get("*", False))
+        self.stream = torch.cuda.current_stream(device) if on else None
         self.ev0 = None
 
     def __enter__(self):
@@ -75,7 +84,7 @@ class _Timed:
         if self.stream is not None and exc[0] is None and _recorder is not None:
             ev1 = torch.cuda.Event(enable_timing=True)
             ev1.record(self.stream)
-            _recorder.setdefault(self.what, []).append((self.ev0, ev1))
+            _recorder.setdefault(self.what, []).append((self.ev0, ev1))  # type: ignore[union-attr]
         return False
 
 
@@ -128,6 +137,14 @@ def load() -> ctypes.CDLL:
     lib.oflow_gru_reset_f32.argtypes = [P, L, P, P, L, P, L, I, I, I, P]
     lib.oflow_gru_blend_f32.restype = I
     lib.oflow_gru_blend_f32.argtypes = [P, L, P, P, L, P, P, L, I, I, I, P]
+    lib.oflow_conv_s32.restype = I
+    lib.oflow_conv_s32.argtypes = [P, L, I, P, I, P, P, I, I, I, I, I, I, I, I, I, F, P, L, P, L, P, L, L, I, P, P, I, P]
+    lib.oflow_pack_s32_f32.restype = I
+    lib.oflow_pack_s32_f32.argtypes = [P, L, I, I, I, I, I, P, L, P, L, P, I, P]
+    lib.oflow_flow_prep_s32.restype = I
+    lib.oflow_flow_prep_s32.argtypes = [P, I, I, I, P, P, L, P, L, P]
+    lib.oflow_corr_lookup_tiled_s32.restype = I
+    lib.oflow_corr_lookup_tiled_s32.argtypes = [PP, IP, IP, I, P, I, I, I, I, P, L, P]
     lib.oflow_corr_lookup_otf_f16.restype = I
     lib.oflow_corr_lookup_otf_f16.argtypes = [P, PP, IP, IP, I, P, I, I, I, I, I, P, P]
     v = lib.oflow_abi_version()
@@ -505,3 +522,190 @@ def gru_blend_(zr: torch.Tensor, bz: torch.Tensor, q: torch.Tensor, bq: torch.Te
             load().oflow_gru_blend_f32(pz, sz, bz.data_ptr(), pq, sq, bq.data_ptr(), ph, sh, h.shape[0], ch, p, _stream(h.device)),
             "gru_blend",
         )
+
+
+# ---- split-fp16 ("S32") update-block path (include/oflow.h; csrc/conv_s32.hip, s32_io.hip) -------------------
+# An S32 activation tensor is fp16 (B, H, W, G, 2, 32): per pixel and 32-channel group one 128-B line holding
+# hi = fp16(v) then lo = fp16(v - hi). A channel slice is ``S32Slice(tensor, g0, ng)``.
+
+
+class S32Slice:
+    """Groups [g0, g0 + ng) of an S32 tensor (a channel slice of a concatenated buffer)."""
+
+    __slots__ = ("t", "g0", "ng")
+
+    def __init__(self, t: torch.Tensor, g0: int = 0, ng: int = -1):
+        if t.dtype != torch.float16 or t.dim() != 6 or tuple(t.shape[-2:]) != (2, 32) or not t.is_contiguous():
+            raise RuntimeError(f"S32 tensor must be contiguous fp16 (B, H, W, G, 2, 32), got {t.dtype} {tuple(t.shape)}")
+        self.t, self.g0 = t, int(g0)
+        self.ng = int(t.shape[3]) - self.g0 if ng < 0 else int(ng)
+        if self.g0 < 0 or self.g0 + self.ng > t.shape[3]:
+            raise RuntimeError("S32Slice: group range outside the tensor")
+
+    @property
+    def ptr(self) -> int:
+        return self.t.data_ptr() + self.g0 * 128
+
+    @property
+    def ps(self) -> int:
+        return int(self.t.shape[3]) * 128
+
+    def channel_ptr(self, c: int) -> int:
+        """Byte address of the hi half of channel c of the slice."""
+        return self.ptr + (c // 32) * 128 + (c % 32) * 2
+
+
+def s32_empty(b: int, h: int, w: int, groups: int, device, zero: bool = False) -> torch.Tensor:
+    f = torch.zeros if zero else torch.empty
+    return f((b, h, w, groups, 2, 32), device=device, dtype=torch.float16)
+
+
+def s32_from_f32(x: torch.Tensor, groups: int = -1) -> torch.Tensor:
+    """(B, C, H, W) fp32 -> S32 tensor (torch ops; test / reference helper, not on the hot path)."""
+    b, c, h, w = x.shape
+    g = (c + 31) // 32 if groups < 0 else groups
+    v = torch.zeros((b, h, w, g * 32), device=x.device, dtype=torch.float32)
+    v[..., :c] = x.permute(0, 2, 3, 1)
+    hi = v.half()
+    lo = (v - hi.float()).half()
+    return torch.stack([hi.view(b, h, w, g, 32), lo.view(b, h, w, g, 32)], dim=4).contiguous()
+
+
+def s32_to_f32(t: torch.Tensor, channels: int = -1) -> torch.Tensor:
+    """S32 tensor -> (B, C, H, W) fp32 = hi + lo."""
+    b, h, w, g = t.shape[:4]
+    v = (t[:, :, :, :, 0].float() + t[:, :, :, :, 1].float()).reshape(b, h, w, g * 32)
+    c = g * 32 if channels < 0 else channels
+    return v[..., :c].permute(0, 3, 1, 2).contiguous()
+
+
+class ConvWeights:
+    """A conv layer's weights packed for oflow_conv_s32: [in_groups][taps][n_pad][hi | lo] fp16 (per-output-channel
+    power-of-two scaled so that max |w| = 2^14 keeps the lo halves normal), the inverse scales and the bias."""
+
+    __slots__ = ("pack", "wscale", "bias", "n", "n_pad", "kh", "kw", "kg")
+
+    def __init__(self, weight: torch.Tensor, bias, n_pad: int, patches7: bool = False):
+        w = weight.detach().float()
+        if patches7:  # 7x7 over 2 channels as a 1x1 over the patch matrix (flow_prep): k = t*2 + c
+            n, c, kh, kw = w.shape
+            w = w.permute(0, 2, 3, 1).reshape(n, kh * kw * c, 1, 1)
+        n, c, kh, kw = w.shape
+        if n_pad < n:
+            raise RuntimeError("ConvWeights: n_pad < out channels")
+        amax = w.abs().amax(dim=(1, 2, 3))
+        e = torch.where(amax > 0, torch.ceil(torch.log2(amax)), torch.zeros_like(amax)).clamp(-100, 100)
+        scale = torch.exp2(14.0 - e)
+        ws = w * scale.view(-1, 1, 1, 1)
+        kg = (c + 31) // 32
+        t = kh * kw
+        full = torch.zeros((n_pad, kg * 32, t), device=w.device, dtype=torch.float32)
+        full[:n, :c] = ws.reshape(n, c, t)
+        full = full.view(n_pad, kg, 32, t).permute(1, 3, 0, 2).contiguous()  # [kg][t][n_pad][32]
+        hi = full.half()
+        lo = (full - hi.float()).half()
+        self.pack = torch.stack([hi, lo], dim=3).contiguous()  # [kg][t][n_pad][2][32]
+        inv = torch.ones(n_pad, device=w.device, dtype=torch.float32)
+        inv[:n] = 1.0 / scale
+        self.wscale = inv
+        self.bias = None if bias is None else bias.detach().float().contiguous()
+        self.n, self.n_pad, self.kh, self.kw, self.kg = n, n_pad, kh, kw, kg
+
+
+def conv_s32(x: S32Slice, cw: ConvWeights, block_n: int, act: str = "none", out_scale: float = 1.0, y0=None, y1=None,
+             f32=None, f32_accumulate: bool = False, epilogue: int = 0, gru_h=None, gru_z=None) -> None:
+    """Split-fp16 convolution (oflow_conv_s32). x: input slice with cw.kg groups. y0/y1: S32Slice destinations.
+    f32: (B, N', H, W) fp32 NCHW destination (channel-contiguous (H, W) planes). epilogue 1/2: GRU gates /
+    candidate with gru_h, gru_z ([P, CH] fp32)."""
+    what = "conv_s32"
+    if x.ng != cw.kg:
+        raise RuntimeError(f"{what}: input has {x.ng} groups, weights expect {cw.kg}")
+    b, h, w = (int(v) for v in x.t.shape[:3])
+    for d in (y0, y1):
+        if d is not None and (tuple(d.t.shape[:3]) != (b, h, w) or d.t.device != x.t.device):
+            raise RuntimeError(f"{what}: destination shape/device mismatch")
+    fp, fbs, fcs = 0, 0, 0
+    if f32 is not None:
+        if f32.dtype != torch.float32 or f32.dim() != 4 or tuple(f32.shape[2:]) != (h, w) or f32.shape[0] != b:
+            raise RuntimeError(f"{what}: fp32 destination must be (B, C, H, W) fp32")
+        if f32.stride(3) != 1 or f32.stride(2) != w or f32.shape[1] < cw.n and epilogue == 0:
+            raise RuntimeError(f"{what}: fp32 destination planes must be contiguous with >= N channels")
+        fp, fbs, fcs = f32.data_ptr(), f32.stride(0), f32.stride(1)
+    gh = gz = 0
+    gch = 0
+    if epilogue:
+        gch = cw.n // 2 if epilogue == 1 else cw.n
+        for tt in (gru_h, gru_z):
+            if tt is None or tt.dtype != torch.float32 or not tt.is_contiguous() or tt.numel() != b * h * w * gch:
+                raise RuntimeError(f"{what}: GRU state tensors must be contiguous fp32 [P, {gch}]")
+        gh, gz = gru_h.data_ptr(), gru_z.data_ptr()
+    dev = x.t.device
+    with torch.cuda.device(dev), _Timed(f"conv{cw.kh}x{cw.kw}", dev):
+        _check(
+            load().oflow_conv_s32(
+                x.ptr, x.ps, cw.kg, cw.pack.data_ptr(), cw.n_pad, cw.wscale.data_ptr(),
+                cw.bias.data_ptr() if cw.bias is not None else None, cw.n, b, h, w, cw.kh, cw.kw, int(block_n),
+                int(epilogue), ACT[act], float(out_scale), y0.ptr if y0 is not None else None, y0.ps if y0 is not None else 0,
+                y1.ptr if y1 is not None else None, y1.ps if y1 is not None else 0, fp or None, fbs, fcs,
+                int(bool(f32_accumulate)), gh or None, gz or None, gch, _stream(dev),
+            ),
+            what,
+        )
+
+
+def pack_s32(x: torch.Tensor, act: str, y0: S32Slice, y1=None, nhwc=None) -> None:
+    """(B, C, H, W) fp32 (a channel slice of a contiguous tensor is fine) -> act -> S32 slices (+ [P, C] fp32)."""
+    what = "pack_s32"
+    if x.device.type != "cuda" or x.dtype != torch.float32 or x.dim() != 4:
+        raise RuntimeError(f"{what}: expected a 4-D fp32 ROCm tensor")
+    b, c, h, w = x.shape
+    if x.stride(3) != 1 or x.stride(2) != w or x.stride(1) != h * w:
+        raise RuntimeError(f"{what}: the (C, H, W) part must be contiguous")
+    if y0.ng * 32 < c or (y1 is not None and y1.ng * 32 < c):
+        raise RuntimeError(f"{what}: destination slice too narrow")
+    if nhwc is not None and (nhwc.dtype != torch.float32 or not nhwc.is_contiguous() or nhwc.numel() != b * h * w * c):
+        raise RuntimeError(f"{what}: nhwc copy must be contiguous fp32 [P, C]")
+    with torch.cuda.device(x.device):
+        _check(
+            load().oflow_pack_s32_f32(
+                x.data_ptr(), x.stride(0), c, b, h, w, ACT[act], y0.ptr, y0.ps, y1.ptr if y1 is not None else None,
+                y1.ps if y1 is not None else 0, nhwc.data_ptr() if nhwc is not None else None, c, _stream(x.device),
+            ),
+            what,
+        )
+
+
+def flow_prep(coords: torch.Tensor, patches: torch.Tensor, flow0=None, flow1=None) -> None:
+    """coords1 (B, 2, H, W) -> convf1 patch matrix (S32, 4 groups) and the flow channels of the GRU inputs.
+    flow0/flow1: (S32Slice, channel) pairs naming where the x flow channel lives (y follows it)."""
+    co = _gpu_f32(coords, "coords", "flow_prep")
+    b, _, h, w = co.shape
+    if tuple(patches.shape) != (b, h, w, 4, 2, 32) or patches.dtype != torch.float16:
+        raise RuntimeError("flow_prep: patches must be S32 (B, H, W, 4, 2, 32)")
+    f0 = (flow0[0].channel_ptr(flow0[1]), flow0[0].ps) if flow0 is not None else (None, 0)
+    f1 = (flow1[0].channel_ptr(flow1[1]), flow1[0].ps) if flow1 is not None else (None, 0)
+    with torch.cuda.device(co.device), _Timed("flow_prep", co.device):
+        _check(load().oflow_flow_prep_s32(co.data_ptr(), b, h, w, patches.data_ptr(), f0[0], f0[1], f1[0], f1[1], _stream(co.device)), "flow_prep")
+
+
+def corr_lookup_tiled_s32(pyr: TiledPyramid, coords: torch.Tensor, radius: int, out: torch.Tensor) -> torch.Tensor:
+    """``corr_lookup_tiled`` written as S32 into ``out`` (B, H, W, G, 2, 32); padding channels are left untouched."""
+    what = "corr_lookup"
+    co = _gpu_f32(coords, "coords", what)
+    b, _, h, w = co.shape
+    nl = len(pyr.levels)
+    k = 2 * int(radius) + 1
+    if b * h * w != pyr.queries:
+        raise RuntimeError(f"{what}: coords {tuple(coords.shape)} do not match the pyramid's {pyr.queries} queries")
+    if out.dtype != torch.float16 or tuple(out.shape[:3]) != (b, h, w) or out.shape[3] * 32 < nl * k * k:
+        raise RuntimeError(f"{what}: S32 output too small")
+    dst = S32Slice(out)
+    ptrs = (ctypes.c_void_p * nl)(*[t.data_ptr() for t in pyr.levels])
+    hs = (ctypes.c_int * nl)(*[d[0] for d in pyr.dims])
+    ws = (ctypes.c_int * nl)(*[d[1] for d in pyr.dims])
+    with torch.cuda.device(co.device), _Timed("corr_lookup", co.device):
+        _check(
+            load().oflow_corr_lookup_tiled_s32(ptrs, hs, ws, nl, co.data_ptr(), b, h, w, int(radius), dst.ptr, dst.ps, _stream(co.device)),
+            what,
+        )
+    return out
