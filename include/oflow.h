@@ -158,12 +158,14 @@ int oflow_gru_blend_f32(const float* d_zr, long long szr, const float* d_bz, con
  *               n >= CH -> sigmoid(.) * d_gru_h[p][n-CH] into S32 d_y0 channel n-CH   (update.py:91-96)
  *   epilogue 2 (GRU candidate, N = CH): h = (1 - z) * h + z * tanh(.), in place in d_gru_h and into S32 d_y0
  *               (update.py:96-97). (act is ignored by epilogues 1 and 2.)
- * oflow_pack_s32_f32: d_x (B, C, H, W) fp32 with batch stride x_batch_stride -> act -> S32 d_y0 (and d_y1), and
- *   optionally a [P][nhwc_pixel_stride] fp32 copy.                       (raft.py:115-118: tanh / relu of cnet)
+ * oflow_pack_s32_f32: d_x (B, C, H, W) fp32 with batch stride x_batch_stride -> act -> S32 d_y0 (and d_y1) channels
+ *   dst_channel + c (dst_channel % 8 == 0; the last 8-channel chunk is zero-filled past C), and optionally a
+ *   [P][nhwc_pixel_stride] fp32 copy.                                     (raft.py:115-118: tanh / relu of cnet)
  * oflow_flow_prep_s32: flow = coords1 - pixel grid (raft.py:129) as the 7x7 patch matrix of convf1
  *   (d_patches: S32 with 4 groups; channel t*2 + c = flow c at tap t = ky*7 + kx, zero padded) and, if not NULL,
  *   the 2 flow channels at d_flow0 / d_flow1 (byte address of the hi half of the x channel; y follows).
- * oflow_corr_lookup_tiled_s32: oflow_corr_lookup_tiled_f32 written as S32 (d_out, out_pixel_stride bytes).
+ * oflow_corr_lookup_tiled_s32: oflow_corr_lookup_tiled_f32 written as S32 (d_out, out_pixel_stride bytes) with
+ *   level l at channels [l*LS, l*LS + (2r+1)^2), LS = (2r+1)^2 rounded up to 8, zeros in the LS - (2r+1)^2 after it.
  */
 int oflow_conv_s32(const void* d_x, long long x_pixel_stride, int in_groups, const void* d_wpack, int n_pad,
                    const float* d_wscale, const float* d_bias, int N, int B, int H, int W, int kh, int kw, int block_n,
@@ -171,8 +173,8 @@ int oflow_conv_s32(const void* d_x, long long x_pixel_stride, int in_groups, con
                    long long y1_pixel_stride, float* d_f32, long long f32_batch_stride, long long f32_channel_stride,
                    int f32_accumulate, float* d_gru_h, float* d_gru_z, int gru_channels, void* stream);
 int oflow_pack_s32_f32(const float* d_x, long long x_batch_stride, int C, int B, int H, int W, int activation,
-                       void* d_y0, long long y0_pixel_stride, void* d_y1, long long y1_pixel_stride, float* d_nhwc,
-                       int nhwc_pixel_stride, void* stream);
+                       int dst_channel, void* d_y0, long long y0_pixel_stride, void* d_y1, long long y1_pixel_stride,
+                       float* d_nhwc, int nhwc_pixel_stride, void* stream);
 int oflow_flow_prep_s32(const float* d_coords, int B, int H, int W, void* d_patches, void* d_flow0,
                         long long flow0_pixel_stride, void* d_flow1, long long flow1_pixel_stride, void* stream);
 int oflow_corr_lookup_tiled_s32(const float* const* d_levels, const int* level_h, const int* level_w, int num_levels,

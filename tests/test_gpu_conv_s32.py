@@ -195,5 +195,11 @@ def test_lookup_s32_equals_lookup(sigma):
     out = N.s32_empty(b, h, w, 11, DEV, zero=True)
     N.corr_lookup_tiled_s32(pyr, coords, 4, out)
     got = N.s32_to_f32(out)
-    assert float((got[:, :324] - ref).abs().max()) <= 2.0 ** -21 * max(1.0, float(ref.abs().max()))
-    assert bool((got[:, 324:] == 0).all())
+    perm = N.lookup_s32_perm(4, 4).to(DEV)
+    assert N.lookup_s32_stride(4) == 88 and perm.numel() == 352
+    real = perm >= 0
+    assert float((got[:, real] - ref[:, perm[real]]).abs().max()) <= 2.0 ** -21 * max(1.0, float(ref.abs().max()))
+    assert bool((got[:, ~real] == 0).all())
+    # the fp32 -> S32 repacking used by the materialised / on-the-fly paths gives the same layout
+    out2 = N.pack_lookup_s32(ref, 4, 4, N.s32_empty(b, h, w, 11, DEV, zero=True))
+    assert torch.equal(out2, out)

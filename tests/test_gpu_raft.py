@@ -104,8 +104,7 @@ class _FixedCorr:
     def lookup_s32(self, coords, out):
         from optical_flow import _native
 
-        _native.pack_s32(self.corrs.pop(0), "none", _native.S32Slice(out))
-        return out
+        return _native.pack_lookup_s32(self.corrs.pop(0), 4, 4, out)
 
 
 def test_split_update_matches_module_update_block():

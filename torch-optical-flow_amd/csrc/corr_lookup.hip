@@ -26,6 +26,10 @@ constexpr int kThreads = 256;
 
 struct LookupArgs {
   const float* lv[OFLOW_MAX_LEVELS];
+  uint8_t* s32;         // S32 output (OUT == 1) and its pixel stride in bytes
+  long long s32ps;
+  int nqb;              // query blocks
+  int nlev;
   int Hl[OFLOW_MAX_LEVELS];
   int Wl[OFLOW_MAX_LEVELS];
   int HB[OFLOW_MAX_LEVELS];  // TILED: ceil(H_l / 4)
@@ -39,7 +43,14 @@ struct LookupArgs {
 
 // TILED: level l stored as [q][H_l/4][W_l/8][4][8] (corr_pyramid.hip, lvl_off): one 4x8 tile = one 128-B line,
 // so a window's row segments share lines with the rows above/below them (fetched once into L2 by this workgroup).
-template <int R, bool TILED>
+// S32 output (OUT = 1; split-fp16 NHWC feeding the update block's convc1, conv_s32.hip): level l occupies channels
+// [l*LS, l*LS + (2r+1)^2), LS = (2r+1)^2 rounded up to 8 (r = 4: 88; 4 levels = 352 = 11 groups), the channels up to
+// the next multiple of 8 are written as zeros; convc1's weights are permuted to match on the host. Every 8-channel
+// chunk belongs to one (query, level): a thread computes 8 window taps and stores one 16-B hi and one 16-B lo half.
+// The 128-B lines straddling two levels are completed by two workgroups: the block -> (query block, level) map puts the
+// levels of one query block on blocks b, b+8, b+16, ... (one XCD under round-robin dispatch, speed only) so that the
+// XCD's L2 merges the two halves before write-back.
+template <int R, bool TILED, int OUT>
 __global__ __launch_bounds__(kThreads) void corr_lookup_kernel(LookupArgs a) {
   constexpr int PK = 2 * R + 2;   // patch side
   constexpr int K = 2 * R + 1;    // window side
@@ -55,8 +66,11 @@ __global__ __launch_bounds__(kThreads) void corr_lookup_kernel(LookupArgs a) {
   __shared__ float4 sW[kQ];
   __shared__ long long sO[kQ];
 
-  const int lvl = blockIdx.y;
-  const int q0 = blockIdx.x * kQ;
+  const int grp = blockIdx.x / (8 * a.nlev), rem = blockIdx.x - grp * 8 * a.nlev;
+  const int lvl = rem >> 3;
+  const int qb = grp * 8 + (rem & 7);
+  if (qb >= a.nqb) return;
+  const int q0 = qb * kQ;
   const int Hl = a.Hl[lvl], Wl = a.Wl[lvl];
   const int HB = a.HB[lvl], WB = a.WB[lvl];
   const float* __restrict__ L = a.lv[lvl];
@@ -121,137 +135,64 @@ __global__ __launch_bounds__(kThreads) void corr_lookup_kernel(LookupArgs a) {
   }
   __syncthreads();
 
-#pragma unroll
-  for (int s = 0; s < PERO; ++s) {
-    const int o = threadIdx.x + kThreads * s;
-    if (o < OUTS) {
-      const int c = o / kQ;
-      const int q = o - c * kQ;
-      const long long off = sO[q];
-      if (off >= 0) {
-        const int i = c / K;           // moves x
-        const int j = c - i * K;       // moves y
-        const float* p = &sP[q * QS + j * PK + i];
-        const float4 w = sW[q];
-        const float val = p[0] * w.x + p[1] * w.y + p[PK] * w.z + p[PK + 1] * w.w;
-        a.out[off + (long long)c * a.N] = val;
-      }
-    }
-  }
-}
-
-// S32 variant (split-fp16 NHWC, conv_s32.hip) feeding the update block's convc1 directly: one workgroup = 64 queries
-// x ALL levels (looped), so the 4 level segments of a pixel's 1408-B output row are written by one workgroup
-// within a few microseconds; lanes walk the channels of one query (2-B hi / lo stores, contiguous runs).
-// Channels L*(2r+1)^2 .. 32*G-1 of the destination are padding and are never written (zeroed once by the host).
-template <int R>
-__global__ __launch_bounds__(kThreads) void corr_lookup_s32_kernel(LookupArgs a, int nlev, uint8_t* out, long long ops) {
-  constexpr int PK = 2 * R + 2;
-  constexpr int K = 2 * R + 1;
-  constexpr int KK = K * K;
-  constexpr int PS = PK * PK;
-  constexpr int QS = PS + 1;
-  constexpr int ITEMS = kQ * PS;
-  constexpr int PER = (ITEMS + kThreads - 1) / kThreads;
-  constexpr int OUTS = kQ * KK;
-  constexpr int PERO = (OUTS + kThreads - 1) / kThreads;
-
-  __shared__ float sP[kQ * QS];
-  __shared__ int sX[kQ], sY[kQ];
-  __shared__ float4 sW[kQ];
-  __shared__ float sC[kQ][2];
-
-  const int q0 = blockIdx.x * kQ;
-  if (threadIdx.x < kQ) {
-    const int q = q0 + threadIdx.x;
-    float cx = 0.f, cy = 0.f;
-    if (q < a.total) {
-      const int b = q / a.N;
-      const int pix = q - b * a.N;
-      cx = a.coords[(size_t)(2 * b) * a.N + pix];
-      cy = a.coords[(size_t)(2 * b + 1) * a.N + pix];
-    }
-    sC[threadIdx.x][0] = cx;
-    sC[threadIdx.x][1] = cy;
-  }
-  for (int lvl = 0; lvl < nlev; ++lvl) {
-    const int Hl = a.Hl[lvl], Wl = a.Wl[lvl];
-    const int HB = a.HB[lvl], WB = a.WB[lvl];
-    const float* __restrict__ L = a.lv[lvl];
-    const float inv = 1.0f / static_cast<float>(1 << lvl);
-    __syncthreads();  // sC written / previous level's patches consumed
-    if (threadIdx.x < kQ) {
-      const float cx = sC[threadIdx.x][0] * inv, cy = sC[threadIdx.x][1] * inv;
-      int xs = -(1 << 28), ys = -(1 << 28);
-      float4 w = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (fabsf(cx) < 4194304.0f && fabsf(cy) < 4194304.0f) {
-        const float fx = floorf(cx), fy = floorf(cy);
-        const float wx = cx - fx, wy = cy - fy;
-        const float ex = 1.0f - wx, ey = 1.0f - wy;
-        xs = static_cast<int>(fx) - R;
-        ys = static_cast<int>(fy) - R;
-        w = make_float4(ey * ex, ey * wx, wy * ex, wy * wx);
-      }
-      sX[threadIdx.x] = xs;
-      sY[threadIdx.x] = ys;
-      sW[threadIdx.x] = w;
-    }
-    __syncthreads();
-    float v[PER];
-#pragma unroll
-    for (int s = 0; s < PER; ++s) {
-      const int item = threadIdx.x + kThreads * s;
-      v[s] = 0.0f;
-      if (item < ITEMS) {
-        const int q = item / PS;
-        const int rem = item - q * PS;
-        const int row = rem / PK;
-        const int col = rem - row * PK;
-        const int y = sY[q] + row, x = sX[q] + col;
-        if (q0 + q < a.total && static_cast<unsigned>(y) < static_cast<unsigned>(Hl) &&
-            static_cast<unsigned>(x) < static_cast<unsigned>(Wl))
-          v[s] = L[(((size_t)(q0 + q) * HB + (y >> 2)) * WB + (x >> 3)) * 32 + ((y & 3) << 3) + (x & 7)];
-      }
-    }
-#pragma unroll
-    for (int s = 0; s < PER; ++s) {
-      const int item = threadIdx.x + kThreads * s;
-      if (item < ITEMS) {
-        const int q = item / PS;
-        sP[q * QS + (item - q * PS)] = v[s];
-      }
-    }
-    __syncthreads();
+  if constexpr (OUT == 0) {
 #pragma unroll
     for (int s = 0; s < PERO; ++s) {
       const int o = threadIdx.x + kThreads * s;
       if (o < OUTS) {
-        const int q = o / KK;
-        const int k = o - q * KK;
-        if (q0 + q < a.total) {
-          const int i = k / K;  // moves x (Q1)
-          const int j = k - i * K;
+        const int c = o / kQ;
+        const int q = o - c * kQ;
+        const long long off = sO[q];
+        if (off >= 0) {
+          const int i = c / K;           // moves x
+          const int j = c - i * K;       // moves y
           const float* p = &sP[q * QS + j * PK + i];
           const float4 w = sW[q];
           const float val = p[0] * w.x + p[1] * w.y + p[PK] * w.z + p[PK + 1] * w.w;
-          const int c = lvl * KK + k;
-          _Float16* line = reinterpret_cast<_Float16*>(out + (long long)(q0 + q) * ops + (c >> 5) * 128) + (c & 31);
-          const _Float16 hi = static_cast<_Float16>(val);
-          line[0] = hi;
-          line[32] = static_cast<_Float16>(val - static_cast<float>(hi));
+          a.out[off + (long long)c * a.N] = val;
         }
       }
+    }
+  } else {
+    typedef _Float16 half8 __attribute__((ext_vector_type(8)));
+    constexpr int KK = K * K, LS = (KK + 7) / 8 * 8, NCH = LS / 8;
+    for (int item = threadIdx.x; item < kQ * NCH; item += kThreads) {
+      const int q = item / NCH;
+      const int ch = item - q * NCH;
+      if (sO[q] < 0) continue;
+      const float4 w = sW[q];
+      half8 hi, lo;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const int k = ch * 8 + e;
+        float val = 0.f;
+        if (k < KK) {
+          const int i = k / K;  // moves x (Q1)
+          const int j = k - i * K;
+          const float* p = &sP[q * QS + j * PK + i];
+          val = p[0] * w.x + p[1] * w.y + p[PK] * w.z + p[PK + 1] * w.w;
+        }
+        const _Float16 h = static_cast<_Float16>(val);
+        hi[e] = h;
+        lo[e] = static_cast<_Float16>(val - static_cast<float>(h));
+      }
+      const int c0 = lvl * LS + ch * 8;
+      uint8_t* line = a.s32 + (long long)(q0 + q) * a.s32ps + (c0 >> 5) * 128 + ((c0 & 31) >> 3) * 16;
+      *reinterpret_cast<half8*>(line) = hi;
+      *reinterpret_cast<half8*>(line + 64) = lo;
     }
   }
 }
 
 template <int R>
-int launch_lookup(const LookupArgs& a, int nlev, hipStream_t s, bool tiled) {
-  dim3 grid((a.total + kQ - 1) / kQ, nlev);
-  if (tiled)
-    hipLaunchKernelGGL((corr_lookup_kernel<R, true>), grid, dim3(kThreads), 0, s, a);
+int launch_lookup(const LookupArgs& a, hipStream_t s, bool tiled, bool s32) {
+  dim3 grid(((a.nqb + 7) / 8) * 8 * a.nlev);
+  if (s32)
+    hipLaunchKernelGGL((corr_lookup_kernel<R, true, 1>), grid, dim3(kThreads), 0, s, a);
+  else if (tiled)
+    hipLaunchKernelGGL((corr_lookup_kernel<R, true, 0>), grid, dim3(kThreads), 0, s, a);
   else
-    hipLaunchKernelGGL((corr_lookup_kernel<R, false>), grid, dim3(kThreads), 0, s, a);
+    hipLaunchKernelGGL((corr_lookup_kernel<R, false, 0>), grid, dim3(kThreads), 0, s, a);
   return launch_status();
 }
 
@@ -262,8 +203,8 @@ using namespace oflow;
 
 static int corr_lookup_impl(const float* const* d_levels, const int* level_h, const int* level_w, int num_levels,
                             const float* d_coords, int B, int H, int W, int radius, float* d_out, void* stream,
-                            bool tiled) {
-  if (!d_levels || !level_h || !level_w || !d_coords || !d_out) return OFLOW_E_NULL;
+                            bool tiled, uint8_t* s32 = nullptr, long long s32ps = 0) {
+  if (!d_levels || !level_h || !level_w || !d_coords || (!d_out && !s32)) return OFLOW_E_NULL;
   if (B <= 0 || H <= 0 || W <= 0) return OFLOW_E_SHAPE;
   if (num_levels < 1 || num_levels > OFLOW_MAX_LEVELS) return OFLOW_E_LEVELS;
   if (radius < 0 || radius > OFLOW_MAX_RADIUS) return OFLOW_E_RADIUS;
@@ -282,19 +223,24 @@ static int corr_lookup_impl(const float* const* d_levels, const int* level_h, co
   const int K = 2 * radius + 1;
   a.coords = d_coords;
   a.out = d_out;
+  a.s32 = s32;
+  a.s32ps = s32ps;
   a.N = H * W;
   a.total = B * H * W;
   a.cout = num_levels * K * K;
+  a.nqb = (a.total + kQ - 1) / kQ;
+  a.nlev = num_levels;
   hipStream_t s = static_cast<hipStream_t>(stream);
+  const bool os = s32 != nullptr;
   switch (radius) {
-    case 0: return launch_lookup<0>(a, num_levels, s, tiled);
-    case 1: return launch_lookup<1>(a, num_levels, s, tiled);
-    case 2: return launch_lookup<2>(a, num_levels, s, tiled);
-    case 3: return launch_lookup<3>(a, num_levels, s, tiled);
-    case 4: return launch_lookup<4>(a, num_levels, s, tiled);
-    case 5: return launch_lookup<5>(a, num_levels, s, tiled);
-    case 6: return launch_lookup<6>(a, num_levels, s, tiled);
-    case 7: return launch_lookup<7>(a, num_levels, s, tiled);
+    case 0: return launch_lookup<0>(a, s, tiled, os);
+    case 1: return launch_lookup<1>(a, s, tiled, os);
+    case 2: return launch_lookup<2>(a, s, tiled, os);
+    case 3: return launch_lookup<3>(a, s, tiled, os);
+    case 4: return launch_lookup<4>(a, s, tiled, os);
+    case 5: return launch_lookup<5>(a, s, tiled, os);
+    case 6: return launch_lookup<6>(a, s, tiled, os);
+    case 7: return launch_lookup<7>(a, s, tiled, os);
     default: return OFLOW_E_RADIUS;
   }
 }
@@ -314,37 +260,12 @@ extern "C" int oflow_corr_lookup_tiled_f32(const float* const* d_levels, const i
 extern "C" int oflow_corr_lookup_tiled_s32(const float* const* d_levels, const int* level_h, const int* level_w,
                                            int num_levels, const float* d_coords, int B, int H, int W, int radius,
                                            void* d_out, long long out_pixel_stride, void* stream) {
-  if (!d_levels || !level_h || !level_w || !d_coords || !d_out) return OFLOW_E_NULL;
-  if (B <= 0 || H <= 0 || W <= 0) return OFLOW_E_SHAPE;
-  if (num_levels < 1 || num_levels > OFLOW_MAX_LEVELS) return OFLOW_E_LEVELS;
+  if (!d_out) return OFLOW_E_NULL;
   if (radius < 0 || radius > OFLOW_MAX_RADIUS) return OFLOW_E_RADIUS;
-  if ((long long)B * H * W >= (1ll << 31) / 64) return OFLOW_E_SHAPE;
+  if (num_levels < 1 || num_levels > OFLOW_MAX_LEVELS) return OFLOW_E_LEVELS;
   const int K = 2 * radius + 1;
-  if (out_pixel_stride < (long long)((num_levels * K * K + 31) / 32) * 128) return OFLOW_E_SHAPE;
+  if (out_pixel_stride < (long long)((num_levels * ((K * K + 7) / 8 * 8) + 31) / 32) * 128) return OFLOW_E_SHAPE;
   if ((out_pixel_stride & 127) || ((uintptr_t)d_out & 15)) return OFLOW_E_ALIGN;
-  LookupArgs a{};
-  for (int l = 0; l < num_levels; ++l) {
-    if (!d_levels[l]) return OFLOW_E_NULL;
-    if (level_h[l] < 2 || level_w[l] < 2) return OFLOW_E_TINY;
-    a.lv[l] = d_levels[l];
-    a.Hl[l] = level_h[l];
-    a.Wl[l] = level_w[l];
-    a.HB[l] = (level_h[l] + 3) / 4;
-    a.WB[l] = (level_w[l] + 7) / 8;
-  }
-  a.coords = d_coords;
-  a.N = H * W;
-  a.total = B * H * W;
-  a.cout = num_levels * K * K;
-  hipStream_t s = static_cast<hipStream_t>(stream);
-  dim3 grid((a.total + kQ - 1) / kQ);
-  uint8_t* out = static_cast<uint8_t*>(d_out);
-  switch (radius) {
-#define OFLOW_CASE(RR) \
-  case RR: hipLaunchKernelGGL((corr_lookup_s32_kernel<RR>), grid, dim3(kThreads), 0, s, a, num_levels, out, out_pixel_stride); break;
-    OFLOW_CASE(0) OFLOW_CASE(1) OFLOW_CASE(2) OFLOW_CASE(3) OFLOW_CASE(4) OFLOW_CASE(5) OFLOW_CASE(6) OFLOW_CASE(7)
-#undef OFLOW_CASE
-    default: return OFLOW_E_RADIUS;
-  }
-  return launch_status();
+  return corr_lookup_impl(d_levels, level_h, level_w, num_levels, d_coords, B, H, W, radius, nullptr, stream, true,
+                          static_cast<uint8_t*>(d_out), out_pixel_stride);
 }

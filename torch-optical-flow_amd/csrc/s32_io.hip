@@ -33,10 +33,11 @@ __device__ __forceinline__ void put8(uint8_t* line, const float* v) {
   *reinterpret_cast<half8*>(line + 64) = lo;
 }
 
-// one thread = one pixel x 8 channels; consecutive threads = consecutive pixels (coalesced NCHW reads)
+// one thread = one pixel x 8 channels; consecutive threads = consecutive pixels (coalesced NCHW reads). Source channel
+// c goes to destination channel yc0 + c (yc0 % 8 == 0); the chunk's channels beyond C are written as zeros.
 __global__ __launch_bounds__(256) void pack_s32_kernel(const float* __restrict__ x, long long xbs, int C, int B, int HW,
-                                                       int act, uint8_t* y0, long long y0ps, uint8_t* y1, long long y1ps,
-                                                       float* f, int fcs) {
+                                                       int act, int yc0, uint8_t* y0, long long y0ps, uint8_t* y1,
+                                                       long long y1ps, float* f, int fcs) {
   const long long P = (long long)B * HW;
   const int C8 = (C + 7) / 8;
   const long long item = (long long)blockIdx.x * blockDim.x + threadIdx.x;
@@ -52,7 +53,8 @@ __global__ __launch_bounds__(256) void pack_s32_kernel(const float* __restrict__
     const int c = c0 + j;
     v[j] = c < C ? act_fn(x[b * xbs + (long long)c * HW + pix], act) : 0.f;
   }
-  const long long off = (long long)(c0 >> 5) * 128 + ((c0 & 31) >> 3) * 16;
+  const int cd = yc0 + c0;  // destination channel (multiple of 8)
+  const long long off = (long long)(cd >> 5) * 128 + ((cd & 31) >> 3) * 16;
   put8(y0 + p * y0ps + off, v);
   if (y1) put8(y1 + p * y1ps + off, v);
   if (f) {
@@ -121,16 +123,16 @@ __global__ __launch_bounds__(256) void flow_prep_kernel(const float* __restrict_
 using namespace oflow;
 
 extern "C" int oflow_pack_s32_f32(const float* d_x, long long x_batch_stride, int C, int B, int H, int W, int activation,
-                                  void* d_y0, long long y0_pixel_stride, void* d_y1, long long y1_pixel_stride,
-                                  float* d_nhwc, int nhwc_pixel_stride, void* stream) {
+                                  int dst_channel, void* d_y0, long long y0_pixel_stride, void* d_y1,
+                                  long long y1_pixel_stride, float* d_nhwc, int nhwc_pixel_stride, void* stream) {
   if (!d_x || !d_y0) return OFLOW_E_NULL;
-  if (B <= 0 || C <= 0 || H <= 0 || W <= 0) return OFLOW_E_SHAPE;
+  if (B <= 0 || C <= 0 || H <= 0 || W <= 0 || dst_channel < 0 || (dst_channel & 7)) return OFLOW_E_SHAPE;
   if (activation < 0 || activation > 3) return OFLOW_E_MODE;
   if ((y0_pixel_stride & 127) || ((uintptr_t)d_y0 & 15) || (d_y1 && ((y1_pixel_stride & 127) || ((uintptr_t)d_y1 & 15))))
     return OFLOW_E_ALIGN;
   const long long items = (long long)B * H * W * ((C + 7) / 8);
   hipLaunchKernelGGL(pack_s32_kernel, dim3((unsigned)((items + 255) / 256)), dim3(256), 0, static_cast<hipStream_t>(stream),
-                     d_x, x_batch_stride, C, B, H * W, activation, static_cast<uint8_t*>(d_y0), y0_pixel_stride,
+                     d_x, x_batch_stride, C, B, H * W, activation, dst_channel, static_cast<uint8_t*>(d_y0), y0_pixel_stride,
                      static_cast<uint8_t*>(d_y1), y1_pixel_stride, d_nhwc, nhwc_pixel_stride);
   return launch_status();
 }

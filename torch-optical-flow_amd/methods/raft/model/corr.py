@@ -48,13 +48,13 @@ class CorrBlock:
         return _native.corr_lookup(self._pyramid, coords, self.radius)
 
     def lookup_s32(self, coords: Tensor, out: Tensor) -> Tensor:
-        """The lookup written as split-fp16 NHWC (S32) into ``out`` for the update block's convc1 (an addition;
-        values equal ``__call__``'s up to the fp16 hi/lo representation of 22 significant bits)."""
+        """The lookup written as split-fp16 NHWC (S32) into ``out`` for the update block's convc1 (an addition):
+        level l at channels [l*LS, l*LS + (2r+1)^2), LS = ``_native.lookup_s32_stride(r)``; values equal
+        ``__call__``'s up to the fp16 hi/lo representation (22 significant bits)."""
         if self._tiled is not None:
             return _native.corr_lookup_tiled_s32(self._tiled, coords, self.radius, out)
         corr = _native.corr_lookup(self._pyramid, coords, self.radius)
-        _native.pack_s32(corr, "none", _native.S32Slice(out))
-        return out
+        return _native.pack_lookup_s32(corr, self.num_levels, self.radius, out)
 
     @staticmethod
     def corr(fmap1: Tensor, fmap2: Tensor) -> Tensor:
@@ -81,6 +81,5 @@ class AlternateCorrBlock:
         return _native.corr_lookup_otf(self.fmap1_f16, self.fmap2_pyramid_f16, coords, self.radius)
 
     def lookup_s32(self, coords: Tensor, out: Tensor) -> Tensor:
-        """``__call__`` repacked as split-fp16 NHWC (S32) into ``out`` for the update block."""
-        _native.pack_s32(self(coords), "none", _native.S32Slice(out))
-        return out
+        """``__call__`` repacked as split-fp16 NHWC (S32, ``_native.lookup_s32_stride`` layout) into ``out``."""
+        return _native.pack_lookup_s32(self(coords), self.num_levels, self.radius, out)

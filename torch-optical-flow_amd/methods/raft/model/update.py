@@ -77,6 +77,7 @@ class BasicUpdateBlock(nn.Module):
 
     def __init__(self, corr_levels: int, corr_radius: int, hidden_dim: int = 128) -> None:
         super().__init__()
+        self.corr_levels, self.corr_radius = corr_levels, corr_radius
         self.encoder = BasicMotionEncoder(corr_levels, corr_radius)
         self.gru = SepConvGRU(hidden_dim=hidden_dim, input_dim=128 + hidden_dim)
         self.flow_head = FlowHead(hidden_dim, hidden_dim=256)
@@ -189,7 +190,8 @@ class SplitUpdate:
         S = _native.s32_empty
         self.hx = S(b, h, w, 12, dev)
         self.rhx = S(b, h, w, 12, dev)
-        self.corr = S(b, h, w, (enc.convc1.in_channels + 31) // 32, dev, zero=True)
+        levels, radius = block.corr_levels, block.corr_radius
+        self.corr = S(b, h, w, (levels * _native.lookup_s32_stride(radius) + 31) // 32, dev, zero=True)
         self.c1 = S(b, h, w, 8, dev)
         self.cf = S(b, h, w, 8, dev)
         self.pm = S(b, h, w, 4, dev)
@@ -211,7 +213,8 @@ class SplitUpdate:
         enc, gru, fh = block.encoder, block.gru, block.flow_head
         CW = _native.ConvWeights
         w = {
-            "c1": CW(enc.convc1.weight, enc.convc1.bias, 256),
+            "c1": CW(enc.convc1.weight, enc.convc1.bias, 256,
+                     in_perm=_native.lookup_s32_perm(block.corr_levels, block.corr_radius)),
             "c2": CW(enc.convc2.weight, enc.convc2.bias, 192),
             "f1": CW(enc.convf1.weight, enc.convf1.bias, 128, patches7=True),
             "f2": CW(enc.convf2.weight, enc.convf2.bias, 64),

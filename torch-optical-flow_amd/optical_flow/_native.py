@@ -140,7 +140,7 @@ def load() -> ctypes.CDLL:
     lib.oflow_conv_s32.restype = I
     lib.oflow_conv_s32.argtypes = [P, L, I, P, I, P, P, I, I, I, I, I, I, I, I, I, F, P, L, P, L, P, L, L, I, P, P, I, P]
     lib.oflow_pack_s32_f32.restype = I
-    lib.oflow_pack_s32_f32.argtypes = [P, L, I, I, I, I, I, P, L, P, L, P, I, P]
+    lib.oflow_pack_s32_f32.argtypes = [P, L, I, I, I, I, I, I, P, L, P, L, P, I, P]
     lib.oflow_flow_prep_s32.restype = I
     lib.oflow_flow_prep_s32.argtypes = [P, I, I, I, P, P, L, P, L, P]
     lib.oflow_corr_lookup_tiled_s32.restype = I
@@ -585,8 +585,12 @@ class ConvWeights:
 
     __slots__ = ("pack", "wscale", "bias", "n", "n_pad", "kh", "kw", "kg")
 
-    def __init__(self, weight: torch.Tensor, bias, n_pad: int, patches7: bool = False):
+    def __init__(self, weight: torch.Tensor, bias, n_pad: int, patches7: bool = False, in_perm=None):
         w = weight.detach().float()
+        if in_perm is not None:  # input channel i of the packing = weight channel in_perm[i] (-1: zero)
+            idx = in_perm.to(w.device)
+            wz = torch.cat([w, torch.zeros_like(w[:, :1])], dim=1)
+            w = wz[:, torch.where(idx < 0, torch.full_like(idx, w.shape[1]), idx)]
         if patches7:  # 7x7 over 2 channels as a 1x1 over the patch matrix (flow_prep): k = t*2 + c
             n, c, kh, kw = w.shape
             w = w.permute(0, 2, 3, 1).reshape(n, kh * kw * c, 1, 1)
@@ -653,26 +657,56 @@ def conv_s32(x: S32Slice, cw: ConvWeights, block_n: int, act: str = "none", out_
         )
 
 
-def pack_s32(x: torch.Tensor, act: str, y0: S32Slice, y1=None, nhwc=None) -> None:
-    """(B, C, H, W) fp32 (a channel slice of a contiguous tensor is fine) -> act -> S32 slices (+ [P, C] fp32)."""
+def pack_s32(x: torch.Tensor, act: str, y0: S32Slice, y1=None, nhwc=None, dst_channel: int = 0) -> None:
+    """(B, C, H, W) fp32 (a channel slice of a contiguous tensor is fine) -> act -> channels dst_channel + c of the S32
+    slices (dst_channel % 8 == 0; the last 8-channel chunk is zero-filled past C), optionally also [P, C] fp32."""
     what = "pack_s32"
     if x.device.type != "cuda" or x.dtype != torch.float32 or x.dim() != 4:
         raise RuntimeError(f"{what}: expected a 4-D fp32 ROCm tensor")
     b, c, h, w = x.shape
     if x.stride(3) != 1 or x.stride(2) != w or x.stride(1) != h * w:
         raise RuntimeError(f"{what}: the (C, H, W) part must be contiguous")
-    if y0.ng * 32 < c or (y1 is not None and y1.ng * 32 < c):
-        raise RuntimeError(f"{what}: destination slice too narrow")
+    need = dst_channel + ((c + 7) // 8) * 8
+    if dst_channel % 8 or y0.ng * 32 < need or (y1 is not None and y1.ng * 32 < need):
+        raise RuntimeError(f"{what}: destination slice too narrow or dst_channel not a multiple of 8")
     if nhwc is not None and (nhwc.dtype != torch.float32 or not nhwc.is_contiguous() or nhwc.numel() != b * h * w * c):
         raise RuntimeError(f"{what}: nhwc copy must be contiguous fp32 [P, C]")
     with torch.cuda.device(x.device):
         _check(
             load().oflow_pack_s32_f32(
-                x.data_ptr(), x.stride(0), c, b, h, w, ACT[act], y0.ptr, y0.ps, y1.ptr if y1 is not None else None,
-                y1.ps if y1 is not None else 0, nhwc.data_ptr() if nhwc is not None else None, c, _stream(x.device),
+                x.data_ptr(), x.stride(0), c, b, h, w, ACT[act], int(dst_channel), y0.ptr, y0.ps,
+                y1.ptr if y1 is not None else None, y1.ps if y1 is not None else 0,
+                nhwc.data_ptr() if nhwc is not None else None, c, _stream(x.device),
             ),
             what,
         )
+
+
+def lookup_s32_stride(radius: int) -> int:
+    """Channels per pyramid level in the S32 lookup layout: (2r+1)^2 rounded up to 8."""
+    k = 2 * int(radius) + 1
+    return (k * k + 7) // 8 * 8
+
+
+def pack_lookup_s32(corr: torch.Tensor, num_levels: int, radius: int, out: torch.Tensor) -> torch.Tensor:
+    """A (B, L*(2r+1)^2, H, W) fp32 lookup output repacked into the S32 lookup layout (level l at l*LS)."""
+    kk = (2 * int(radius) + 1) ** 2
+    ls = lookup_s32_stride(radius)
+    dst = S32Slice(out)
+    for lvl in range(num_levels):
+        pack_s32(corr[:, lvl * kk : (lvl + 1) * kk], "none", dst, dst_channel=lvl * ls)
+    return out
+
+
+def lookup_s32_perm(num_levels: int, radius: int) -> torch.Tensor:
+    """Input-channel map of the S32 lookup layout: entry l*LS + k = l*(2r+1)^2 + k, -1 for the padding channels
+    (used to permute convc1's weights, ConvWeights(in_perm=...))."""
+    kk = (2 * int(radius) + 1) ** 2
+    ls = lookup_s32_stride(radius)
+    perm = torch.full((num_levels * ls,), -1, dtype=torch.long)
+    for lvl in range(num_levels):
+        perm[lvl * ls : lvl * ls + kk] = torch.arange(lvl * kk, (lvl + 1) * kk)
+    return perm
 
 
 def flow_prep(coords: torch.Tensor, patches: torch.Tensor, flow0=None, flow1=None) -> None:
@@ -689,7 +723,8 @@ def flow_prep(coords: torch.Tensor, patches: torch.Tensor, flow0=None, flow1=Non
 
 
 def corr_lookup_tiled_s32(pyr: TiledPyramid, coords: torch.Tensor, radius: int, out: torch.Tensor) -> torch.Tensor:
-    """``corr_lookup_tiled`` written as S32 into ``out`` (B, H, W, G, 2, 32); padding channels are left untouched."""
+    """``corr_lookup_tiled`` written as S32 into ``out`` (B, H, W, G, 2, 32): level l at channels [l*LS, l*LS + (2r+1)^2)
+    (LS = lookup_s32_stride(r)), zeros after each level; channels past L*LS are left untouched."""
     what = "corr_lookup"
     co = _gpu_f32(coords, "coords", what)
     b, _, h, w = co.shape
@@ -697,7 +732,7 @@ def corr_lookup_tiled_s32(pyr: TiledPyramid, coords: torch.Tensor, radius: int, 
     k = 2 * int(radius) + 1
     if b * h * w != pyr.queries:
         raise RuntimeError(f"{what}: coords {tuple(coords.shape)} do not match the pyramid's {pyr.queries} queries")
-    if out.dtype != torch.float16 or tuple(out.shape[:3]) != (b, h, w) or out.shape[3] * 32 < nl * k * k:
+    if out.dtype != torch.float16 or tuple(out.shape[:3]) != (b, h, w) or out.shape[3] * 32 < nl * lookup_s32_stride(radius):
         raise RuntimeError(f"{what}: S32 output too small")
     dst = S32Slice(out)
     ptrs = (ctypes.c_void_p * nl)(*[t.data_ptr() for t in pyr.levels])
