@@ -17,6 +17,7 @@
  *                              + methods/raft/model/utils.py:64-80 (bilinear_sampler)
  *   oflow_grid_warp_f32     <- optical_flow/operator/operator.py:8-56 (warp, warp_grid -> F.grid_sample)
  *   oflow_conv_s32 & co.    <- methods/raft/model/update.py:40-161 (update-block convolutions)
+ *   oflow_stem_patches_s32, oflow_norm_*, oflow_conv_s32_ex <- methods/raft/model/extractor.py:35-231 (encoders)
  */
 #ifndef OFLOW_H_
 #define OFLOW_H_
@@ -180,6 +181,39 @@ int oflow_flow_prep_s32(const float* d_coords, int B, int H, int W, void* d_patc
 int oflow_corr_lookup_tiled_s32(const float* const* d_levels, const int* level_h, const int* level_w, int num_levels,
                                 const float* d_coords, int B, int H, int W, int radius, void* d_out,
                                 long long out_pixel_stride, void* stream);
+
+/*
+ * Encoders on the split-fp16 path (methods/raft/model/extractor.py:35-231; csrc/encoder_s32.hip).
+ *
+ * oflow_conv_s32_ex: oflow_conv_s32 plus (epilogue 0 only)
+ *   d_nhwc        : fp32 [P][nhwc_pixel_stride] copy of the value (after activation / residual);
+ *   d_stats       : per-tile instance-norm partials (count, mean, M2) of the pre-activation conv output, layout
+ *                   [B][ceil(H/4)*ceil(W/32)][n_pad][3] floats (reduced by oflow_norm_stats_finalize);
+ *   d_res         : S32 residual added after the activation, then res_activation (relu(x + y), extractor.py:90);
+ *   s2d           : S32 destinations in space-to-depth layout (pixel (y/2, x/2), channel + ((y%2)*2 + x%2) * N), the
+ *                   input form of the next stage's stride-2 convolutions (a 3x3/2 conv = a 2x2/1 conv on s2d input,
+ *                   a 1x1/2 conv = a 1x1 conv over the first N channels of it).  kh x kw also allows 2x2 (taps at
+ *                   offsets -1, 0), block_n also 96.
+ * oflow_stem_patches_s32: 7x7/2 pad-3 patch matrix of a (B, C, H, W) fp32 image: S32 (B, ceil(H/2), ceil(W/2),
+ *   out_groups) with channel t*C + c (t = ky*7 + kx), zeros past 49*C.
+ * oflow_norm_stats_finalize: merge the partials (fp64) -> alpha = 1/sqrt(var + eps), beta = -mean * alpha, [B][C].
+ * oflow_norm_apply_s32: y = act(x*alpha + beta) for x [P][C] fp32 (C % 8 == 0); res_mode 1: y = res_act(y + S32 res),
+ *   res_mode 2: y = res_act((x2*alpha2 + beta2) + y); written as S32 (s2d: space-to-depth as above).
+ */
+int oflow_conv_s32_ex(const void* d_x, long long x_pixel_stride, int in_groups, const void* d_wpack, int n_pad,
+                      const float* d_wscale, const float* d_bias, int N, int B, int H, int W, int kh, int kw,
+                      int block_n, int epilogue, int activation, float out_scale, void* d_y0, long long y0_pixel_stride,
+                      void* d_y1, long long y1_pixel_stride, float* d_f32, long long f32_batch_stride,
+                      long long f32_channel_stride, int f32_accumulate, float* d_gru_h, float* d_gru_z,
+                      int gru_channels, float* d_nhwc, int nhwc_pixel_stride, float* d_stats, const void* d_res,
+                      long long res_pixel_stride, int res_activation, int s2d, void* stream);
+int oflow_stem_patches_s32(const float* d_img, int B, int C, int H, int W, void* d_out, int out_groups, void* stream);
+int oflow_norm_stats_finalize(const float* d_partials, int B, int tiles, int n_pad, int C, double eps, float* d_alpha,
+                              float* d_beta, void* stream);
+int oflow_norm_apply_s32(const float* d_x, int C, int B, int H, int W, const float* d_alpha, const float* d_beta,
+                         int activation, int res_mode, const void* d_res, long long res_pixel_stride, const float* d_x2,
+                         const float* d_alpha2, const float* d_beta2, int res_activation, int s2d, void* d_y,
+                         long long y_pixel_stride, void* stream);
 
 #ifdef __cplusplus
 }

@@ -28,7 +28,7 @@ def _epe(a, b):
     return float(e.mean()), float(e.max())
 
 
-@pytest.mark.parametrize("impl", ["split", "fused"])
+@pytest.mark.parametrize("impl", ["split", "fused", "split+module-encoders"])
 @pytest.mark.parametrize("tag", ["small", "small24", "kittimode", "sintel", "kitti"])
 def test_raft_matches_reference_flows(golden, tag, impl):
     g = golden("raft_e2e")
@@ -37,7 +37,9 @@ def test_raft_matches_reference_flows(golden, tag, impl):
     padder = InputPadder(img0.shape, mode=str(g[f"{tag}_mode"]))
     p0, p1 = (x.to(DEV) for x in padder.pad(img0, img1))
     model = _model(RAFT)
-    model.update_impl = impl
+    model.update_impl = impl.split("+")[0]
+    if impl.endswith("module-encoders") or impl == "fused":
+        model.encoder_impl = "module"
     with torch.inference_mode():
         low, up = model(p0, p1, iters=iters, test_mode=True)
     up = padder.unpad(up)[..., ::s, ::s]
@@ -139,3 +141,32 @@ def test_split_update_matches_module_update_block():
         err = float((ref - got).abs().max())
         print(f"{what}: max |d| {err:.2e}")
         assert err <= 1e-4 * max(1.0, float(ref.abs().max())), (what, err)
+
+
+@pytest.mark.parametrize("norm", ["instance", "batch"])
+@pytest.mark.parametrize("b,h,w", [(2, 128, 160), (2, 440, 1024)])
+def test_split_encoder_matches_module(norm, b, h, w):
+    """SplitEncoder (split-fp16 convs, fp64-merged instance-norm statistics / folded eval batch norm, space-to-depth
+    stride-2 stages) against the nn.Module encoder (MIOpen fp32) on the same GPU."""
+    from model.extractor import BasicEncoder, SplitEncoder
+
+    model = _model(RAFT)
+    enc = model.fnet if norm == "instance" else model.cnet
+    if norm == "batch":  # non-trivial running statistics and affine parameters
+        g = torch.Generator().manual_seed(1)
+        for m in enc.modules():
+            if isinstance(m, torch.nn.BatchNorm2d):
+                m.running_mean.copy_(torch.randn(m.num_features, generator=g) * 0.1)
+                m.running_var.copy_(torch.rand(m.num_features, generator=g) + 0.5)
+                m.weight.data.copy_(torch.rand(m.num_features, generator=g) + 0.5)
+                m.bias.data.copy_(torch.randn(m.num_features, generator=g) * 0.1)
+    img0, img1 = synthetic.synthetic_pair(b, h, w, seed=2)
+    x = (2 * (img0.to(DEV) / 255.0) - 1.0).contiguous()
+    with torch.inference_mode():
+        ref = enc(x)
+        got = SplitEncoder(enc)(x)
+    err = float((got - ref).abs().max())
+    scale = float(ref.abs().max())
+    print(f"{norm} {b}x{h}x{w}: max |d| {err:.2e} (max |ref| {scale:.2f})")
+    assert got.shape == ref.shape
+    assert err <= 1e-4 * max(1.0, scale), err

@@ -58,6 +58,14 @@ struct ConvArgs {
   float* h;
   float* z;
   int gch;
+  // encoder options (EPI 0)
+  float* fn;               // fp32 NHWC destination [P][fnps] (pre-activation value when stats are taken) or null
+  int fnps;
+  float* stats;            // per-tile (count, mean, M2) partials [B][tiles][npad][3] of the conv output, or null
+  const uint8_t* res;      // S32 residual added after the activation (then res_act), or null
+  long long resps;
+  int res_act;
+  int s2d;                 // S32 destinations in space-to-depth layout: pixel (y/2, x/2), channel + ((y&1)*2+(x&1))*N
 };
 
 __device__ __forceinline__ float act_fn(float v, int act) {
@@ -260,7 +268,39 @@ __global__ __launch_bounds__(kThreads, 2) void conv_s32_kernel(ConvArgs a) {
       }
     }
   }
-  if (a.y0 == nullptr && EPI == 0) return;
+  if constexpr (EPI == 0) {
+    if (a.stats != nullptr && tid < BN) {
+      // per-tile instance-norm partials of the conv output (Chan et al. merge in oflow_norm_stats_finalize)
+      const int n = n0 + tid;
+      if (n < a.N) {
+        const float ws = a.wsc[n], bi = a.bias ? a.bias[n] : 0.f;
+        int cnt = 0;
+        float sum = 0.f;
+        for (int pl = 0; pl < kBM; ++pl) {
+          const int y = ty0 + pl / kTX, x = tx0 + (pl % kTX);
+          if (y < a.H && x < a.W) {
+            sum += sT[pl * TS + tid] * ws + bi;
+            ++cnt;
+          }
+        }
+        const float mean = sum / static_cast<float>(cnt);
+        float m2 = 0.f;
+        for (int pl = 0; pl < kBM; ++pl) {
+          const int y = ty0 + pl / kTX, x = tx0 + (pl % kTX);
+          if (y < a.H && x < a.W) {
+            const float d = sT[pl * TS + tid] * ws + bi - mean;
+            m2 += d * d;
+          }
+        }
+        const int tile_in_img = (ty0 / kTY) * a.tiles_x + tx0 / kTX;
+        float* st = a.stats + (((long long)b * a.tiles_x * a.tiles_y + tile_in_img) * a.npad + n) * 3;
+        st[0] = static_cast<float>(cnt);
+        st[1] = mean;
+        st[2] = m2;
+      }
+    }
+    if (a.y0 == nullptr && a.fn == nullptr) return;
+  }
 
   // S32 / GRU consumers: one thread = one pixel x 8 consecutive channels
   constexpr int C8 = BN / 8;
@@ -281,8 +321,37 @@ __global__ __launch_bounds__(kThreads, 2) void conv_s32_kernel(ConvArgs a) {
     if constexpr (EPI == 0) {
 #pragma unroll
       for (int j = 0; j < 8; ++j) v[j] = act_fn(v[j], a.act) * a.oscale;
-      store_s32(a.y0, a.y0ps, P, n, a.N, v);
-      if (a.y1) store_s32(a.y1, a.y1ps, P, n, a.N, v);
+      if (a.res) {
+        const uint8_t* rl = a.res + P * a.resps + (long long)(n >> 5) * 128 + ((n & 31) >> 3) * 16;
+        const half8 rh = *reinterpret_cast<const half8*>(rl), rlo = *reinterpret_cast<const half8*>(rl + 64);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          v[j] = v[j] + (static_cast<float>(rh[j]) + static_cast<float>(rlo[j]));
+          if (a.res_act) v[j] = act_fn(v[j], a.res_act);
+        }
+      }
+      if (a.fn) {
+        float* fp = a.fn + P * a.fnps + n;
+        if (n + 8 <= a.N) {
+          *reinterpret_cast<float4*>(fp) = make_float4(v[0], v[1], v[2], v[3]);
+          *reinterpret_cast<float4*>(fp + 4) = make_float4(v[4], v[5], v[6], v[7]);
+        } else {
+#pragma unroll
+          for (int j = 0; j < 8; ++j)
+            if (n + j < a.N) fp[j] = v[j];
+        }
+      }
+      if (a.y0) {
+        long long Pd = P;
+        int nd = n;
+        if (a.s2d) {
+          const int W2 = a.W >> 1, H2 = a.H >> 1;
+          Pd = ((long long)b * H2 + (y >> 1)) * W2 + (x >> 1);
+          nd = n + ((y & 1) * 2 + (x & 1)) * a.N;
+        }
+        store_s32(a.y0, a.y0ps, Pd, nd, a.s2d ? 4 * a.N : a.N, v);
+        if (a.y1) store_s32(a.y1, a.y1ps, Pd, nd, a.s2d ? 4 * a.N : a.N, v);
+      }
     } else if constexpr (EPI == 1) {
       // [z | r] gates (update.py:91-96): z = sigmoid -> a.z; r*h = sigmoid(r) * h -> S32 y0 (channel n - gch)
       if (n < a.gch) {
@@ -325,6 +394,7 @@ template <int KH, int KW, int EPI>
 int launch_bn(const ConvArgs& a, int bn, hipStream_t s) {
   switch (bn) {
     case 128: return launch_conv<KH, KW, 128, 2, 2, EPI>(a, s);
+    case 96: return launch_conv<KH, KW, 96, 4, 1, EPI>(a, s);
     case 64: return launch_conv<KH, KW, 64, 2, 2, EPI>(a, s);
     case 32: return launch_conv<KH, KW, 32, 4, 1, EPI>(a, s);
     default: return OFLOW_E_SHAPE;
@@ -336,22 +406,29 @@ int launch_bn(const ConvArgs& a, int bn, hipStream_t s) {
 
 using namespace oflow;
 
-extern "C" int oflow_conv_s32(const void* d_x, long long x_pixel_stride, int in_groups, const void* d_wpack, int n_pad,
-                              const float* d_wscale, const float* d_bias, int N, int B, int H, int W, int kh, int kw,
-                              int block_n, int epilogue, int activation, float out_scale, void* d_y0,
-                              long long y0_pixel_stride, void* d_y1, long long y1_pixel_stride, float* d_f32,
-                              long long f32_batch_stride, long long f32_channel_stride, int f32_accumulate,
-                              float* d_gru_h, float* d_gru_z, int gru_channels, void* stream) {
+extern "C" int oflow_conv_s32_ex(const void* d_x, long long x_pixel_stride, int in_groups, const void* d_wpack,
+                                 int n_pad, const float* d_wscale, const float* d_bias, int N, int B, int H, int W, int kh,
+                                 int kw, int block_n, int epilogue, int activation, float out_scale, void* d_y0,
+                                 long long y0_pixel_stride, void* d_y1, long long y1_pixel_stride, float* d_f32,
+                                 long long f32_batch_stride, long long f32_channel_stride, int f32_accumulate,
+                                 float* d_gru_h, float* d_gru_z, int gru_channels, float* d_nhwc, int nhwc_pixel_stride,
+                                 float* d_stats, const void* d_res, long long res_pixel_stride, int res_activation,
+                                 int s2d, void* stream) {
   if (!d_x || !d_wpack || !d_wscale) return OFLOW_E_NULL;
   if (B <= 0 || H <= 0 || W <= 0 || N <= 0 || in_groups <= 0 || n_pad < N || n_pad % block_n) return OFLOW_E_SHAPE;
-  if (activation < 0 || activation > 3 || epilogue < 0 || epilogue > 2) return OFLOW_E_MODE;
+  if (activation < 0 || activation > 3 || res_activation < 0 || res_activation > 3 || epilogue < 0 || epilogue > 2)
+    return OFLOW_E_MODE;
   if ((x_pixel_stride & 127) || ((uintptr_t)d_x & 15) || ((uintptr_t)d_wpack & 15)) return OFLOW_E_ALIGN;
-  if (epilogue == 0 && !d_y0 && !d_f32) return OFLOW_E_NULL;
+  if (epilogue == 0 && !d_y0 && !d_f32 && !d_nhwc && !d_stats) return OFLOW_E_NULL;
   if (epilogue != 0 && (!d_y0 || !d_gru_h || !d_gru_z || gru_channels <= 0 || gru_channels % 8)) return OFLOW_E_NULL;
   if (epilogue == 1 && N != 2 * gru_channels) return OFLOW_E_SHAPE;
   if (epilogue == 2 && N != gru_channels) return OFLOW_E_SHAPE;
+  if (epilogue != 0 && (d_nhwc || d_stats || d_res || s2d)) return OFLOW_E_MODE;
+  if (s2d && ((H | W) & 1 || N % 8)) return OFLOW_E_SHAPE;
+  if (d_nhwc && (nhwc_pixel_stride < N || ((uintptr_t)d_nhwc & 15) || (nhwc_pixel_stride & 3))) return OFLOW_E_ALIGN;
   if ((d_y0 && ((y0_pixel_stride & 127) || ((uintptr_t)d_y0 & 15))) ||
-      (d_y1 && ((y1_pixel_stride & 127) || ((uintptr_t)d_y1 & 15))))
+      (d_y1 && ((y1_pixel_stride & 127) || ((uintptr_t)d_y1 & 15))) ||
+      (d_res && ((res_pixel_stride & 127) || ((uintptr_t)d_res & 15))))
     return OFLOW_E_ALIGN;
   ConvArgs a{};
   a.x = static_cast<const uint8_t*>(d_x);
@@ -380,12 +457,20 @@ extern "C" int oflow_conv_s32(const void* d_x, long long x_pixel_stride, int in_
   a.h = d_gru_h;
   a.z = d_gru_z;
   a.gch = gru_channels;
+  a.fn = d_nhwc;
+  a.fnps = nhwc_pixel_stride;
+  a.stats = d_stats;
+  a.res = static_cast<const uint8_t*>(d_res);
+  a.resps = res_pixel_stride;
+  a.res_act = res_activation;
+  a.s2d = s2d;
   hipStream_t s = static_cast<hipStream_t>(stream);
   const int key = kh * 16 + kw;
   switch (epilogue) {
     case 0:
       switch (key) {
         case 0x11: return launch_bn<1, 1, 0>(a, block_n, s);
+        case 0x22: return launch_bn<2, 2, 0>(a, block_n, s);
         case 0x33: return launch_bn<3, 3, 0>(a, block_n, s);
         case 0x15: return launch_bn<1, 5, 0>(a, block_n, s);
         case 0x51: return launch_bn<5, 1, 0>(a, block_n, s);
@@ -402,4 +487,16 @@ extern "C" int oflow_conv_s32(const void* d_x, long long x_pixel_stride, int in_
       if (key == 0x51) return launch_conv<5, 1, 128, 2, 2, 2>(a, s);
       return OFLOW_E_SHAPE;
   }
+}
+
+extern "C" int oflow_conv_s32(const void* d_x, long long x_pixel_stride, int in_groups, const void* d_wpack, int n_pad,
+                              const float* d_wscale, const float* d_bias, int N, int B, int H, int W, int kh, int kw,
+                              int block_n, int epilogue, int activation, float out_scale, void* d_y0,
+                              long long y0_pixel_stride, void* d_y1, long long y1_pixel_stride, float* d_f32,
+                              long long f32_batch_stride, long long f32_channel_stride, int f32_accumulate,
+                              float* d_gru_h, float* d_gru_z, int gru_channels, void* stream) {
+  return oflow_conv_s32_ex(d_x, x_pixel_stride, in_groups, d_wpack, n_pad, d_wscale, d_bias, N, B, H, W, kh, kw,
+                           block_n, epilogue, activation, out_scale, d_y0, y0_pixel_stride, d_y1, y1_pixel_stride,
+                           d_f32, f32_batch_stride, f32_channel_stride, f32_accumulate, d_gru_h, d_gru_z, gru_channels,
+                           nullptr, 0, nullptr, nullptr, 0, 0, 0, stream);
 }

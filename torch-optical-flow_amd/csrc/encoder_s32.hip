@@ -1,0 +1,208 @@
+// Feature / context encoder stages around the split-fp16 convolution (conv_s32.hip) (gfx950).
+//
+// Replaces the non-convolution parts of methods/raft/model/extractor.py:35-231 (BasicEncoder, ResidualBlock):
+//   oflow_stem_patches_s32   : the 7x7 / stride 2 / pad 3 stem's patch matrix (extractor.py:186) as S32, channel
+//                              t*C + c = input channel c at tap t = ky*7 + kx (C = 3: 147 channels, zero padded to 160),
+//                              so the stem runs as a 1x1 split-fp16 GEMM.
+//   oflow_norm_stats_finalize: instance-norm statistics (nn.InstanceNorm2d, extractor.py:22, biased variance, eps) of a
+//                              convolution output from the per-tile (count, mean, M2) partials its epilogue wrote,
+//                              merged in fp64 (Chan et al.), as the affine form the reference applies:
+//                              y = x * invstd + (-mean * invstd)  (ATen batch_norm_cpu_transform_input).
+//   oflow_norm_apply_s32     : y = act(x * alpha[b,c] + beta[b,c]) [+ residual, act2] -> S32 (optionally space-to-depth),
+//                              i.e. relu(norm(conv)) and the block tail relu(x + y) / relu(norm3(down) + y)
+//                              (extractor.py:76-90).
+#include "oflow_internal.h"
+
+namespace oflow {
+namespace {
+
+typedef _Float16 half8 __attribute__((ext_vector_type(8)));
+
+__device__ __forceinline__ float act_fn(float v, int act) {
+  if (act == 1) return v < 0.f ? 0.f : v;
+  if (act == 2) return 1.0f / (1.0f + expf(-v));
+  if (act == 3) return tanhf(v);
+  return v;
+}
+
+__device__ __forceinline__ void put8(uint8_t* line, const float* v) {
+  half8 hi, lo;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const _Float16 a = static_cast<_Float16>(v[j]);
+    hi[j] = a;
+    lo[j] = static_cast<_Float16>(v[j] - static_cast<float>(a));
+  }
+  *reinterpret_cast<half8*>(line) = hi;
+  *reinterpret_cast<half8*>(line + 64) = lo;
+}
+
+// one thread = one output pixel x one 32-channel group of the patch matrix
+__global__ __launch_bounds__(256) void stem_patches_kernel(const float* __restrict__ img, int B, int C, int H, int W,
+                                                           int Ho, int Wo, int G, uint8_t* out) {
+  constexpr int KS = 7, PAD = 3, ST = 2;
+  const long long P = (long long)B * Ho * Wo;
+  const long long item = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (item >= P * G) return;
+  const int g = static_cast<int>(item % G);
+  const long long p = item / G;
+  const int b = static_cast<int>(p / ((long long)Ho * Wo));
+  const int pix = static_cast<int>(p - (long long)b * Ho * Wo);
+  const int oy = pix / Wo, ox = pix - oy * Wo;
+  const float* src = img + (long long)b * C * H * W;
+  float v[32];
+#pragma unroll
+  for (int e = 0; e < 32; ++e) {
+    const int k = g * 32 + e;
+    const int t = k / C, c = k - t * C;
+    float val = 0.f;
+    if (t < KS * KS) {
+      const int iy = oy * ST - PAD + t / KS, ix = ox * ST - PAD + t % KS;
+      if (static_cast<unsigned>(iy) < static_cast<unsigned>(H) && static_cast<unsigned>(ix) < static_cast<unsigned>(W))
+        val = src[((long long)c * H + iy) * W + ix];
+    }
+    v[e] = val;
+  }
+  uint8_t* line = out + (p * G + g) * 128;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) put8(line + q * 16, v + 8 * q);
+}
+
+// one workgroup = one image x 64 channels: lane = channel (coalesced 12-B partials), the 4 waves stride over the tiles,
+// each lane merges its tiles in fp64 (Chan et al.), then the 4 wave results are merged through LDS
+__global__ __launch_bounds__(256) void norm_stats_kernel(const float* __restrict__ part, int B, int tiles, int npad, int C,
+                                                         double eps, float* alpha, float* beta) {
+  __shared__ double sN[4][64], sM[4][64], sQ[4][64];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int cblocks = (C + 63) / 64;
+  const int b = blockIdx.x / cblocks, c = (blockIdx.x - b * cblocks) * 64 + lane;
+  double n = 0.0, mean = 0.0, m2 = 0.0;
+  if (c < C) {
+    for (int t = wave; t < tiles; t += 4) {
+      const float* p = part + (((long long)b * tiles + t) * npad + c) * 3;
+      const double nb = p[0];
+      if (nb <= 0.0) continue;
+      const double mb = p[1], m2b = p[2];
+      const double nn = n + nb;
+      const double d = mb - mean;
+      mean += d * nb / nn;
+      m2 += m2b + d * d * n * nb / nn;
+      n = nn;
+    }
+  }
+  sN[wave][lane] = n;
+  sM[wave][lane] = mean;
+  sQ[wave][lane] = m2;
+  __syncthreads();
+  if (wave == 0 && c < C) {
+    for (int w = 1; w < 4; ++w) {
+      const double nb = sN[w][lane];
+      if (nb <= 0.0) continue;
+      const double nn = n + nb;
+      const double d = sM[w][lane] - mean;
+      mean += d * nb / nn;
+      m2 += sQ[w][lane] + d * d * n * nb / nn;
+      n = nn;
+    }
+    const double var = n > 0.0 ? m2 / n : 0.0;
+    const float invstd = static_cast<float>(1.0 / sqrt(var + eps));
+    alpha[(long long)b * C + c] = invstd;
+    beta[(long long)b * C + c] = -static_cast<float>(mean) * invstd;
+  }
+}
+
+// one thread = one pixel x 8 channels
+__global__ __launch_bounds__(256) void norm_apply_kernel(const float* __restrict__ x, int C, int B, int H, int W,
+                                                         const float* __restrict__ alpha, const float* __restrict__ beta,
+                                                         int act, int res_mode, const uint8_t* res, long long resps,
+                                                         const float* __restrict__ x2, const float* __restrict__ alpha2,
+                                                         const float* __restrict__ beta2, int res_act, int s2d,
+                                                         uint8_t* y, long long yps) {
+  const int C8 = C / 8;
+  const long long P = (long long)B * H * W;
+  const long long item = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (item >= P * C8) return;
+  const int c8 = static_cast<int>(item % C8);
+  const long long p = item / C8;
+  const int b = static_cast<int>(p / ((long long)H * W));
+  const int c0 = c8 * 8;
+  const float4* xp = reinterpret_cast<const float4*>(x + p * C + c0);
+  const float4 u0 = xp[0], u1 = xp[1];
+  float v[8] = {u0.x, u0.y, u0.z, u0.w, u1.x, u1.y, u1.z, u1.w};
+  const float* al = alpha + (long long)b * C + c0;
+  const float* be = beta + (long long)b * C + c0;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) v[j] = act_fn(v[j] * al[j] + be[j], act);
+  if (res_mode == 1) {  // S32 residual (identity shortcut)
+    const uint8_t* rl = res + p * resps + (long long)(c0 >> 5) * 128 + ((c0 & 31) >> 3) * 16;
+    const half8 rh = *reinterpret_cast<const half8*>(rl), rlo = *reinterpret_cast<const half8*>(rl + 64);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = act_fn(v[j] + (static_cast<float>(rh[j]) + static_cast<float>(rlo[j])), res_act);
+  } else if (res_mode == 2) {  // normalised raw residual (downsample branch: norm3(conv1x1(x)))
+    const float4* rp = reinterpret_cast<const float4*>(x2 + p * C + c0);
+    const float4 r0 = rp[0], r1 = rp[1];
+    const float r[8] = {r0.x, r0.y, r0.z, r0.w, r1.x, r1.y, r1.z, r1.w};
+    const float* a2 = alpha2 + (long long)b * C + c0;
+    const float* b2 = beta2 + (long long)b * C + c0;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = act_fn((r[j] * a2[j] + b2[j]) + v[j], res_act);
+  }
+  long long pd = p;
+  int cd = c0;
+  if (s2d) {
+    const int pix = static_cast<int>(p - (long long)b * H * W);
+    const int yy = pix / W, xx = pix - yy * W;
+    pd = ((long long)b * (H >> 1) + (yy >> 1)) * (W >> 1) + (xx >> 1);
+    cd = c0 + ((yy & 1) * 2 + (xx & 1)) * C;
+  }
+  put8(y + pd * yps + (long long)(cd >> 5) * 128 + ((cd & 31) >> 3) * 16, v);
+}
+
+}  // namespace
+}  // namespace oflow
+
+using namespace oflow;
+
+extern "C" int oflow_stem_patches_s32(const float* d_img, int B, int C, int H, int W, void* d_out, int out_groups,
+                                      void* stream) {
+  if (!d_img || !d_out) return OFLOW_E_NULL;
+  if (B <= 0 || C <= 0 || H <= 0 || W <= 0 || out_groups * 32 < 49 * C) return OFLOW_E_SHAPE;
+  if ((uintptr_t)d_out & 15) return OFLOW_E_ALIGN;
+  const int Ho = (H - 1) / 2 + 1, Wo = (W - 1) / 2 + 1;  // (H + 2*3 - 7) / 2 + 1
+  const long long items = (long long)B * Ho * Wo * out_groups;
+  hipLaunchKernelGGL(stem_patches_kernel, dim3((unsigned)((items + 255) / 256)), dim3(256), 0,
+                     static_cast<hipStream_t>(stream), d_img, B, C, H, W, Ho, Wo, out_groups, static_cast<uint8_t*>(d_out));
+  return launch_status();
+}
+
+extern "C" int oflow_norm_stats_finalize(const float* d_partials, int B, int tiles, int n_pad, int C, double eps,
+                                         float* d_alpha, float* d_beta, void* stream) {
+  if (!d_partials || !d_alpha || !d_beta) return OFLOW_E_NULL;
+  if (B <= 0 || tiles <= 0 || C <= 0 || n_pad < C) return OFLOW_E_SHAPE;
+  hipLaunchKernelGGL(norm_stats_kernel, dim3(B * ((C + 63) / 64)), dim3(256), 0, static_cast<hipStream_t>(stream),
+                     d_partials, B, tiles, n_pad, C, eps, d_alpha, d_beta);
+  return launch_status();
+}
+
+extern "C" int oflow_norm_apply_s32(const float* d_x, int C, int B, int H, int W, const float* d_alpha,
+                                    const float* d_beta, int activation, int res_mode, const void* d_res,
+                                    long long res_pixel_stride, const float* d_x2, const float* d_alpha2,
+                                    const float* d_beta2, int res_activation, int s2d, void* d_y,
+                                    long long y_pixel_stride, void* stream) {
+  if (!d_x || !d_alpha || !d_beta || !d_y) return OFLOW_E_NULL;
+  if (B <= 0 || C <= 0 || C % 8 || H <= 0 || W <= 0) return OFLOW_E_SHAPE;
+  if (activation < 0 || activation > 3 || res_activation < 0 || res_activation > 3 || res_mode < 0 || res_mode > 2)
+    return OFLOW_E_MODE;
+  if (res_mode == 1 && !d_res) return OFLOW_E_NULL;
+  if (res_mode == 2 && (!d_x2 || !d_alpha2 || !d_beta2)) return OFLOW_E_NULL;
+  if (s2d && ((H | W) & 1)) return OFLOW_E_SHAPE;
+  if (((uintptr_t)d_x & 15) || ((uintptr_t)d_y & 15) || (y_pixel_stride & 127) ||
+      (d_res && (((uintptr_t)d_res & 15) || (res_pixel_stride & 127))) || (d_x2 && ((uintptr_t)d_x2 & 15)))
+    return OFLOW_E_ALIGN;
+  const long long items = (long long)B * H * W * (C / 8);
+  hipLaunchKernelGGL(norm_apply_kernel, dim3((unsigned)((items + 255) / 256)), dim3(256), 0, static_cast<hipStream_t>(stream),
+                     d_x, C, B, H, W, d_alpha, d_beta, activation, res_mode, static_cast<const uint8_t*>(d_res),
+                     res_pixel_stride, d_x2, d_alpha2, d_beta2, res_activation, s2d, static_cast<uint8_t*>(d_y),
+                     y_pixel_stride);
+  return launch_status();
+}

@@ -1,8 +1,10 @@
 """Feature / context encoders (reference: methods/raft/model/extractor.py:35-231).
 
-Caller-side of the hot path: the convolutions run on PyTorch-ROCm (MIOpen), not on custom kernels in this
-build. Parameter names and registration order equal the reference's, so reference
-``state_dict``s load unchanged. ``SmallEncoder``/``BottleneckBlock`` (never instantiated by RAFT,
+``BasicEncoder``/``ResidualBlock`` are the nn.Modules (parameter names and registration order equal the
+reference's, so reference ``state_dict``s load unchanged). For GPU inference RAFT runs them through
+``SplitEncoder``: every convolution on the split-fp16 matrix-core kernel (csrc/conv_s32.hip), instance norm from
+per-tile partials merged in fp64, batch norm (eval) folded into the convolutions, ReLU / residual adds fused, and the
+stride-2 stages fed in space-to-depth layout. ``SmallEncoder``/``BottleneckBlock`` (never instantiated by RAFT,
 `raft.py:40-47`) are not provided.
 """
 from __future__ import annotations
@@ -12,6 +14,8 @@ from typing import List, Sequence, Tuple, Union
 import torch
 import torch.nn as nn
 from torch import Tensor
+
+from optical_flow import _native
 
 
 def _norm_layer(norm_fn: str, planes: int, groups: int) -> nn.Module:
@@ -94,3 +98,156 @@ class BasicEncoder(nn.Module):
         if is_list:
             return torch.split(x, [batch_dim, batch_dim], dim=0)
         return x
+
+
+# ---- split-fp16 inference path ---------------------------------------------------------------------------------
+
+
+def _s2d_weight(w: Tensor) -> Tensor:
+    """(N, C, 3, 3) stride-2 pad-1 weights -> (N, 4C, 2, 2) stride-1 weights over the space-to-depth input (channel
+    (a*2 + b)*C + c = input pixel (2Y + a, 2X + b)); taps at offsets -1, 0: ky = 2*ky' + a - 1."""
+    n, c = w.shape[:2]
+    out = torch.zeros((n, 4, c, 2, 2), device=w.device, dtype=w.dtype)
+    for kyp in range(2):
+        for a in range(2):
+            ky = 2 * kyp + a - 1
+            if not 0 <= ky <= 2:
+                continue
+            for kxp in range(2):
+                for b in range(2):
+                    kx = 2 * kxp + b - 1
+                    if 0 <= kx <= 2:
+                        out[:, a * 2 + b, :, kyp, kxp] = w[:, :, ky, kx]
+    return out.reshape(n, 4 * c, 2, 2)
+
+
+def _fold_bn(conv: nn.Conv2d, bn: nn.Module):
+    """Eval-mode BatchNorm after a conv folded into it (ATen: y = x*alpha + beta, alpha = gamma/sqrt(var + eps),
+    beta = beta - mean*alpha), computed in fp64."""
+    w = conv.weight.detach().double()
+    b = conv.bias.detach().double() if conv.bias is not None else torch.zeros(w.shape[0], device=w.device, dtype=w.dtype)
+    alpha = bn.weight.detach().double() / torch.sqrt(bn.running_var.detach().double() + bn.eps)
+    beta = bn.bias.detach().double() - bn.running_mean.detach().double() * alpha
+    return (w * alpha.view(-1, 1, 1, 1)).float(), (b * alpha + beta).float()
+
+
+class SplitEncoder:
+    """Inference execution of a ``BasicEncoder`` (norm 'instance' or 'batch' in eval mode) on the split-fp16 kernels.
+
+    Activations are S32 (split-fp16 NHWC, include/oflow.h). Instance norm: each conv writes its fp32 NHWC output plus
+    per-tile (count, mean, M2) partials; ``oflow_norm_stats_finalize`` merges them in fp64 and ``oflow_norm_apply_s32``
+    applies x*invstd - mean*invstd, the ReLU and the block's residual tail. Batch norm: folded into the conv, ReLU and
+    the residual add run in the conv epilogue. Stride-2 3x3 convs run as 2x2 convs on the space-to-depth layout that
+    the previous stage writes directly; their 1x1 stride-2 shortcuts read its first C channels. The stem is a 1x1 GEMM
+    over the 7x7 patch matrix.
+    """
+
+    def __init__(self, enc: BasicEncoder) -> None:
+        if enc.norm_fn not in ("instance", "batch"):
+            raise RuntimeError(f"SplitEncoder: norm_fn {enc.norm_fn!r} not supported")
+        if enc.norm_fn == "batch" and enc.training:
+            raise RuntimeError("SplitEncoder: batch norm needs eval mode (running statistics)")
+        self.enc = enc
+        self.inorm = enc.norm_fn == "instance"
+        key = tuple((q.data_ptr(), q._version) for q in enc.parameters()) + tuple(
+            (q.data_ptr(), q._version) for q in enc.buffers()
+        )
+        cache = enc.__dict__.get("_split_weights")
+        if cache is None or cache[0] != key:
+            enc.__dict__["_split_weights"] = (key, self._pack(enc))
+        self.w = enc.__dict__["_split_weights"][1]
+
+    def _cw(self, conv: nn.Conv2d, norm, **kw):
+        if self.inorm or norm is None:
+            w, b = conv.weight, conv.bias
+        else:
+            w, b = _fold_bn(conv, norm)
+        if kw.pop("s2d", False):
+            w = _s2d_weight(w.detach().float())
+        n = w.shape[0]
+        return _native.ConvWeights(w, b, ((n + 31) // 32) * 32, **kw)
+
+    def _pack(self, enc: BasicEncoder):
+        W = {"stem": self._cw(enc.conv1, enc.norm1, patches=True)}
+        for li, layer in enumerate((enc.layer1, enc.layer2, enc.layer3)):
+            for bi, blk in enumerate(layer):
+                s2 = blk.downsample is not None
+                W[f"{li}.{bi}.conv1"] = self._cw(blk.conv1, blk.norm1, s2d=s2)
+                W[f"{li}.{bi}.conv2"] = self._cw(blk.conv2, blk.norm2)
+                if s2:
+                    W[f"{li}.{bi}.down"] = self._cw(blk.downsample[0], blk.downsample[1])
+        W["head"] = _native.ConvWeights(enc.conv2.weight, enc.conv2.bias, ((enc.conv2.out_channels + 31) // 32) * 32)
+        return W
+
+    @staticmethod
+    def _bn(n: int) -> int:
+        return {64: 64, 96: 96, 128: 128}.get(n, 128 if n % 128 == 0 else 64 if n % 64 == 0 else 32)
+
+    def _conv_norm(self, x, cw, shape, act, out=None, res=None, s2d=False, raw_only=False):
+        """conv -> norm -> act [-> + res -> relu]: returns the S32 output (or (raw, alpha, beta) when raw_only)."""
+        b, h, w = shape
+        bn = self._bn(cw.n)
+        V = _native.S32Slice
+        if self.inorm:
+            raw = torch.empty((b * h * w, cw.n), device=x.t.device, dtype=torch.float32)
+            tiles = _native.conv_tiles(h, w)
+            part = torch.empty((b, tiles, cw.n_pad, 3), device=x.t.device, dtype=torch.float32)
+            _native.conv_s32(x, cw, bn, nhwc=raw, stats=part)
+            alpha, beta = _native.norm_stats(part, b, tiles, cw.n_pad, cw.n, 1e-5)
+            if raw_only:
+                return raw, alpha, beta
+            if out is None:
+                out = _native.s32_empty(b, h // 2 if s2d else h, w // 2 if s2d else w, (cw.n * (4 if s2d else 1) + 31) // 32, x.t.device)
+            if isinstance(res, tuple):
+                _native.norm_apply(raw, (b, cw.n, h, w), alpha, beta, act, V(out), res_raw=res, res_act="relu", s2d=s2d)
+            else:
+                _native.norm_apply(raw, (b, cw.n, h, w), alpha, beta, act, V(out), res=res, res_act="relu" if res is not None else "none", s2d=s2d)
+            return out
+        if raw_only:
+            out = _native.s32_empty(b, h, w, (cw.n + 31) // 32, x.t.device)
+            _native.conv_s32(x, cw, bn, y0=V(out))
+            return out
+        if out is None:
+            out = _native.s32_empty(b, h // 2 if s2d else h, w // 2 if s2d else w, (cw.n * (4 if s2d else 1) + 31) // 32, x.t.device)
+        _native.conv_s32(x, cw, bn, act=act, y0=V(out), res=res, res_act="relu" if res is not None else "none", s2d=s2d)
+        return out
+
+    def __call__(self, x: Union[Tensor, Sequence[Tensor]]) -> Union[Tensor, Tuple[Tensor, ...]]:
+        is_list = isinstance(x, (tuple, list))
+        if is_list:
+            batch_dim = x[0].shape[0]
+            x = torch.cat(list(x), dim=0)
+        x = x.float().contiguous()
+        n, _, hh, ww = x.shape
+        if hh % 8 or ww % 8:
+            raise RuntimeError("SplitEncoder: H and W must be multiples of 8")
+        V = _native.S32Slice
+        dev = x.device
+        h, w = hh // 2, ww // 2
+        patches = _native.s32_empty(n, h, w, self.w["stem"].kg, dev)
+        _native.stem_patches(x, patches)
+        cur = self._conv_norm(V(patches), self.w["stem"], (n, h, w), "relu")
+        layers = (self.enc.layer1, self.enc.layer2, self.enc.layer3)
+        for li, layer in enumerate(layers):
+            for bi, blk in enumerate(layer):
+                last_of_stage = bi == len(layer) - 1
+                out_s2d = last_of_stage and li + 1 < len(layers)  # the next stage starts with stride-2 convs
+                pre = f"{li}.{bi}."
+                if blk.downsample is None:
+                    t = self._conv_norm(V(cur), self.w[pre + "conv1"], (n, h, w), "relu")
+                    cur = self._conv_norm(V(t), self.w[pre + "conv2"], (n, h, w), "relu", res=V(cur), s2d=out_s2d)
+                else:
+                    h, w = h // 2, w // 2  # cur is the space-to-depth input at the new resolution
+                    t = self._conv_norm(V(cur), self.w[pre + "conv1"], (n, h, w), "relu")
+                    cin = self.w[pre + "down"].kg
+                    d = self._conv_norm(V(cur, 0, cin), self.w[pre + "down"], (n, h, w), "none", raw_only=True)
+                    res = d if self.inorm else V(d)
+                    cur = self._conv_norm(V(t), self.w[pre + "conv2"], (n, h, w), "relu", res=res, s2d=out_s2d)
+                if out_s2d:
+                    pass  # cur now holds (n, h/2, w/2, 4C) for the next stage
+        head = self.w["head"]
+        out = torch.empty((n, head.n, h, w), device=dev, dtype=torch.float32)
+        _native.conv_s32(V(cur), head, self._bn(head.n), f32=out)
+        if is_list:
+            return torch.split(out, [batch_dim, batch_dim], dim=0)
+        return out

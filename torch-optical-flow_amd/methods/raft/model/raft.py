@@ -10,7 +10,9 @@ values; three output-identical changes remove host work from the loop:
   * coordinate grids are built on the device (no CPU build + H2D copy, `raft.py:68-69`);
   * with ``test_mode=True`` only the last iteration's convex upsampling is computed — the reference computes
     all ``iters`` and returns only the last (Q11, `raft.py:136-145`);
-  * without autograd on the GPU the update block runs through ``SplitUpdate``: every convolution on the
+  * without autograd on the GPU the encoders run through ``SplitEncoder`` (split-fp16 convolutions, fp64-merged
+    instance-norm statistics, folded eval batch norm; ``encoder_impl = "module"`` keeps the nn.Modules) and the
+    update block runs through ``SplitUpdate``: every convolution on the
     split-fp16 matrix-core kernel (fp32-level accuracy) with the GRU gates, activations, concatenations and the
     ``coords1 += delta_flow`` update fused into convolution epilogues (``update_impl = "fused"`` selects the
     MIOpen-based ``FusedUpdate`` instead); in test mode the mask head (two convolutions feeding only the
@@ -27,7 +29,7 @@ import torch.nn.functional as F
 from torch import Tensor
 
 from .corr import AlternateCorrBlock, CorrBlock
-from .extractor import BasicEncoder
+from .extractor import BasicEncoder, SplitEncoder
 from .update import BasicUpdateBlock, FusedUpdate, SplitUpdate
 from .utils import coords_grid, upflow8
 
@@ -86,6 +88,8 @@ class RAFT(nn.Module):
         # elementwise kernels (FusedUpdate); "module": the nn.Module as written. fused_update=False forces "module".
         self.update_impl = "split"
         self.fused_update = True
+        # "split": encoders on the split-fp16 kernels (SplitEncoder) in GPU inference; "module": nn.Module (MIOpen)
+        self.encoder_impl = "split"
 
     # -- checkpoints -------------------------------------------------------------------------------------
     @classmethod
@@ -143,11 +147,14 @@ class RAFT(nn.Module):
         image1 = (2 * (image1 / 255.0) - 1.0).contiguous()
         hdim, cdim = self.hparams.hidden_dim, self.hparams.context_dim
 
-        fmap1, fmap2 = self.fnet([image0, image1])
+        split_enc = image0.is_cuda and not torch.is_grad_enabled() and self.encoder_impl == "split"
+        fnet = SplitEncoder(self.fnet) if split_enc else self.fnet
+        cnet = SplitEncoder(self.cnet) if split_enc and not self.cnet.training else self.cnet
+        fmap1, fmap2 = fnet([image0, image1])
         block = AlternateCorrBlock if self.hparams.get("alternate_corr", False) else CorrBlock
         corr_fn = block(fmap1.float(), fmap2.float(), radius=self.hparams.corr_radius)
 
-        cnet_out = self.cnet(image0)
+        cnet_out = cnet(image0)
         coords0, coords1 = self.initialize_flow(image0)
         if flow_init is not None:
             coords1 = coords1 + flow_init

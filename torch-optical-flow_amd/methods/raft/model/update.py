@@ -216,7 +216,7 @@ class SplitUpdate:
             "c1": CW(enc.convc1.weight, enc.convc1.bias, 256,
                      in_perm=_native.lookup_s32_perm(block.corr_levels, block.corr_radius)),
             "c2": CW(enc.convc2.weight, enc.convc2.bias, 192),
-            "f1": CW(enc.convf1.weight, enc.convf1.bias, 128, patches7=True),
+            "f1": CW(enc.convf1.weight, enc.convf1.bias, 128, patches=True),
             "f2": CW(enc.convf2.weight, enc.convf2.bias, 64),
             "mo": CW(enc.conv.weight, enc.conv.bias, 128),
             "fh1": CW(fh.conv1.weight, fh.conv1.bias, 256),

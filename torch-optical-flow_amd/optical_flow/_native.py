@@ -48,6 +48,10 @@ SYMBOLS = (
     "oflow_pack_s32_f32",
     "oflow_flow_prep_s32",
     "oflow_corr_lookup_tiled_s32",
+    "oflow_conv_s32_ex",
+    "oflow_stem_patches_s32",
+    "oflow_norm_stats_finalize",
+    "oflow_norm_apply_s32",
 )
 
 _lib = None
@@ -139,6 +143,15 @@ def load() -> ctypes.CDLL:
     lib.oflow_gru_blend_f32.argtypes = [P, L, P, P, L, P, P, L, I, I, I, P]
     lib.oflow_conv_s32.restype = I
     lib.oflow_conv_s32.argtypes = [P, L, I, P, I, P, P, I, I, I, I, I, I, I, I, I, F, P, L, P, L, P, L, L, I, P, P, I, P]
+    lib.oflow_conv_s32_ex.restype = I
+    lib.oflow_conv_s32_ex.argtypes = [P, L, I, P, I, P, P, I, I, I, I, I, I, I, I, I, F, P, L, P, L, P, L, L, I, P, P, I,
+                                      P, I, P, P, L, I, I, P]
+    lib.oflow_stem_patches_s32.restype = I
+    lib.oflow_stem_patches_s32.argtypes = [P, I, I, I, I, P, I, P]
+    lib.oflow_norm_stats_finalize.restype = I
+    lib.oflow_norm_stats_finalize.argtypes = [P, I, I, I, I, ctypes.c_double, P, P, P]
+    lib.oflow_norm_apply_s32.restype = I
+    lib.oflow_norm_apply_s32.argtypes = [P, I, I, I, I, P, P, I, I, P, L, P, P, P, I, I, P, L, P]
     lib.oflow_pack_s32_f32.restype = I
     lib.oflow_pack_s32_f32.argtypes = [P, L, I, I, I, I, I, I, P, L, P, L, P, I, P]
     lib.oflow_flow_prep_s32.restype = I
@@ -585,13 +598,13 @@ class ConvWeights:
 
     __slots__ = ("pack", "wscale", "bias", "n", "n_pad", "kh", "kw", "kg")
 
-    def __init__(self, weight: torch.Tensor, bias, n_pad: int, patches7: bool = False, in_perm=None):
+    def __init__(self, weight: torch.Tensor, bias, n_pad: int, patches: bool = False, in_perm=None):
         w = weight.detach().float()
         if in_perm is not None:  # input channel i of the packing = weight channel in_perm[i] (-1: zero)
             idx = in_perm.to(w.device)
             wz = torch.cat([w, torch.zeros_like(w[:, :1])], dim=1)
             w = wz[:, torch.where(idx < 0, torch.full_like(idx, w.shape[1]), idx)]
-        if patches7:  # 7x7 over 2 channels as a 1x1 over the patch matrix (flow_prep): k = t*2 + c
+        if patches:  # kh x kw conv as a 1x1 over its patch matrix (flow_prep, stem_patches): channel k = t*C + c
             n, c, kh, kw = w.shape
             w = w.permute(0, 2, 3, 1).reshape(n, kh * kw * c, 1, 1)
         n, c, kh, kw = w.shape
@@ -616,18 +629,28 @@ class ConvWeights:
         self.n, self.n_pad, self.kh, self.kw, self.kg = n, n_pad, kh, kw, kg
 
 
+def conv_tiles(h: int, w: int) -> int:
+    """Output tiles (4 rows x 32 columns) per image of oflow_conv_s32: the instance-norm partials' tile count."""
+    return ((h + 3) // 4) * ((w + 31) // 32)
+
+
 def conv_s32(x: S32Slice, cw: ConvWeights, block_n: int, act: str = "none", out_scale: float = 1.0, y0=None, y1=None,
-             f32=None, f32_accumulate: bool = False, epilogue: int = 0, gru_h=None, gru_z=None) -> None:
-    """Split-fp16 convolution (oflow_conv_s32). x: input slice with cw.kg groups. y0/y1: S32Slice destinations.
-    f32: (B, N', H, W) fp32 NCHW destination (channel-contiguous (H, W) planes). epilogue 1/2: GRU gates /
-    candidate with gru_h, gru_z ([P, CH] fp32)."""
+             f32=None, f32_accumulate: bool = False, epilogue: int = 0, gru_h=None, gru_z=None, nhwc=None, stats=None,
+             res=None, res_act: str = "none", s2d: bool = False) -> None:
+    """Split-fp16 convolution (oflow_conv_s32_ex). x: input slice with cw.kg groups. y0/y1: S32Slice destinations
+    (s2d: space-to-depth layout, half the spatial size). f32: (B, N', H, W) fp32 NCHW destination. nhwc: [P, N]
+    fp32 destination. stats: instance-norm partials [B, conv_tiles(H, W), n_pad, 3]. res: S32Slice residual added
+    after the activation, then res_act. epilogue 1/2: GRU gates / candidate with gru_h, gru_z ([P, CH] fp32)."""
     what = "conv_s32"
     if x.ng != cw.kg:
         raise RuntimeError(f"{what}: input has {x.ng} groups, weights expect {cw.kg}")
     b, h, w = (int(v) for v in x.t.shape[:3])
+    hw_out = (h // 2, w // 2) if s2d else (h, w)
     for d in (y0, y1):
-        if d is not None and (tuple(d.t.shape[:3]) != (b, h, w) or d.t.device != x.t.device):
+        if d is not None and (tuple(d.t.shape[:3]) != (b, *hw_out) or d.t.device != x.t.device):
             raise RuntimeError(f"{what}: destination shape/device mismatch")
+    if res is not None and (tuple(res.t.shape[:3]) != (b, h, w) or res.ng * 32 < cw.n):
+        raise RuntimeError(f"{what}: residual shape mismatch")
     fp, fbs, fcs = 0, 0, 0
     if f32 is not None:
         if f32.dtype != torch.float32 or f32.dim() != 4 or tuple(f32.shape[2:]) != (h, w) or f32.shape[0] != b:
@@ -635,6 +658,10 @@ def conv_s32(x: S32Slice, cw: ConvWeights, block_n: int, act: str = "none", out_
         if f32.stride(3) != 1 or f32.stride(2) != w or f32.shape[1] < cw.n and epilogue == 0:
             raise RuntimeError(f"{what}: fp32 destination planes must be contiguous with >= N channels")
         fp, fbs, fcs = f32.data_ptr(), f32.stride(0), f32.stride(1)
+    if nhwc is not None and (nhwc.dtype != torch.float32 or not nhwc.is_contiguous() or nhwc.numel() != b * h * w * cw.n):
+        raise RuntimeError(f"{what}: nhwc destination must be contiguous fp32 [P, {cw.n}]")
+    if stats is not None and (stats.dtype != torch.float32 or stats.numel() < b * conv_tiles(h, w) * cw.n_pad * 3):
+        raise RuntimeError(f"{what}: stats partials buffer too small")
     gh = gz = 0
     gch = 0
     if epilogue:
@@ -646,14 +673,63 @@ def conv_s32(x: S32Slice, cw: ConvWeights, block_n: int, act: str = "none", out_
     dev = x.t.device
     with torch.cuda.device(dev), _Timed(f"conv{cw.kh}x{cw.kw}", dev):
         _check(
-            load().oflow_conv_s32(
+            load().oflow_conv_s32_ex(
                 x.ptr, x.ps, cw.kg, cw.pack.data_ptr(), cw.n_pad, cw.wscale.data_ptr(),
                 cw.bias.data_ptr() if cw.bias is not None else None, cw.n, b, h, w, cw.kh, cw.kw, int(block_n),
                 int(epilogue), ACT[act], float(out_scale), y0.ptr if y0 is not None else None, y0.ps if y0 is not None else 0,
                 y1.ptr if y1 is not None else None, y1.ps if y1 is not None else 0, fp or None, fbs, fcs,
-                int(bool(f32_accumulate)), gh or None, gz or None, gch, _stream(dev),
+                int(bool(f32_accumulate)), gh or None, gz or None, gch,
+                nhwc.data_ptr() if nhwc is not None else None, cw.n,
+                stats.data_ptr() if stats is not None else None,
+                res.ptr if res is not None else None, res.ps if res is not None else 0, ACT[res_act], int(bool(s2d)),
+                _stream(dev),
             ),
             what,
+        )
+
+
+def stem_patches(img: torch.Tensor, out: torch.Tensor) -> torch.Tensor:
+    """7x7 / stride 2 / pad 3 patch matrix of a (B, C, H, W) fp32 image as S32 (channel t*C + c)."""
+    x = _gpu_f32(img, "image", "stem_patches")
+    b, c, h, w = x.shape
+    if out.dtype != torch.float16 or tuple(out.shape[:3]) != (b, (h + 1) // 2, (w + 1) // 2):
+        raise RuntimeError("stem_patches: output must be S32 (B, ceil(H/2), ceil(W/2), G, 2, 32)")
+    with torch.cuda.device(x.device), _Timed("stem_patches", x.device):
+        _check(load().oflow_stem_patches_s32(x.data_ptr(), b, c, h, w, out.data_ptr(), int(out.shape[3]), _stream(x.device)), "stem_patches")
+    return out
+
+
+def norm_stats(partials: torch.Tensor, b: int, tiles: int, n_pad: int, c: int, eps: float):
+    """Per-(image, channel) instance-norm affine (alpha = 1/sqrt(var + eps), beta = -mean * alpha) from partials."""
+    alpha = torch.empty((b, c), device=partials.device, dtype=torch.float32)
+    beta = torch.empty_like(alpha)
+    with torch.cuda.device(partials.device):
+        _check(
+            load().oflow_norm_stats_finalize(partials.data_ptr(), b, tiles, n_pad, c, float(eps), alpha.data_ptr(), beta.data_ptr(), _stream(partials.device)),
+            "norm_stats",
+        )
+    return alpha, beta
+
+
+def norm_apply(x: torch.Tensor, shape, alpha, beta, act: str, y: S32Slice, res=None, res_raw=None, res_act: str = "none",
+               s2d: bool = False) -> None:
+    """y = act(x*alpha + beta) (+ residual, res_act) as S32. x: [P, C] fp32 (NHWC). res: S32Slice (identity shortcut);
+    res_raw: (x2 [P, C], alpha2, beta2) normalised shortcut."""
+    b, c, h, w = shape
+    mode, rp, rps = 0, None, 0
+    x2 = a2 = b2 = None
+    if res is not None:
+        mode, rp, rps = 1, res.ptr, res.ps
+    elif res_raw is not None:
+        mode = 2
+        x2, a2, b2 = (t.data_ptr() for t in res_raw)
+    with torch.cuda.device(x.device), _Timed("norm_apply", x.device):
+        _check(
+            load().oflow_norm_apply_s32(
+                x.data_ptr(), c, b, h, w, alpha.data_ptr(), beta.data_ptr(), ACT[act], mode, rp, rps, x2, a2, b2,
+                ACT[res_act], int(bool(s2d)), y.ptr, y.ps, _stream(x.device),
+            ),
+            "norm_apply",
         )
 
 
