@@ -196,7 +196,7 @@ int oflow_corr_lookup_tiled_s32(const float* const* d_levels, const int* level_h
  *                   offsets -1, 0), block_n also 96.
  * oflow_stem_patches_s32: 7x7/2 pad-3 patch matrix of a (B, C, H, W) fp32 image: S32 (B, ceil(H/2), ceil(W/2),
  *   out_groups) with channel t*C + c (t = ky*7 + kx), zeros past 49*C.
- * oflow_norm_stats_finalize: merge the partials (fp64) -> alpha = 1/sqrt(var + eps), beta = -mean * alpha, [B][C].
+ * oflow_norm_stats_finalize: merge the partials (fp64 sums) -> alpha = 1/sqrt(var + eps), beta = -mean * alpha, [B][C].
  * oflow_norm_apply_s32: y = act(x*alpha + beta) for x [P][C] fp32 (C % 8 == 0); res_mode 1: y = res_act(y + S32 res),
  *   res_mode 2: y = res_act((x2*alpha2 + beta2) + y); written as S32 (s2d: space-to-depth as above).
  */
