@@ -46,6 +46,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--shape", default="sintel8", choices=sorted(SHAPES))
     ap.add_argument("--iters", type=int, default=30)
+    ap.add_argument("--layer", default=None, help="only layers whose name contains this string (PMC runs)")
+    ap.add_argument("--no-lookup", action="store_true")
     args = ap.parse_args()
     b, h, w = SHAPES[args.shape]
     dev = torch.device("cuda", 0)
@@ -79,6 +81,8 @@ def main():
     out = {"shape": args.shape, "layers": {}}
     total = 0.0
     for name, kh, kw, cin, n, npad, bn, gi, go, epi in layers:
+        if args.layer and args.layer not in name:
+            continue
         x = s32(gi)
         cw = weights(n, cin, kh, kw, npad)
         kw_ = {}
@@ -98,6 +102,9 @@ def main():
             "mfma_frac": round(padded / (ms * 1e-3) / F16_PEAK, 3),
         }
     out["update_iteration_convs_us"] = round(total * 1e3, 1)
+    if args.no_lookup:
+        print(json.dumps(out, indent=1))
+        return
     # S32 lookup (and the NCHW one) on a real pyramid
     f1, f2 = synthetic.synthetic_fmaps(b, 256, h, w, stream=3)
     f1, f2 = f1.to(dev), f2.to(dev)

@@ -106,8 +106,10 @@ __device__ __forceinline__ void store_s32(uint8_t* y, long long ps, long long P,
   }
 }
 
-template <int KH, int KW, int BN, int WM, int WN, int EPI>
-__global__ __launch_bounds__(kThreads, 2) void conv_s32_kernel(ConvArgs a) {
+// VAR (experiment hooks, 0 in the product): bit 0 s_setprio(1) around each MFMA block; bit 1 issue both K-halves'
+// LDS operand reads before the MFMAs; bit 2 ask for 3 waves per SIMD.
+template <int KH, int KW, int BN, int WM, int WN, int EPI, int VAR = 0>
+__global__ __launch_bounds__(kThreads, (VAR & 4) ? 3 : 2) void conv_s32_kernel(ConvArgs a) {
   constexpr int T = KH * KW;
   constexpr int PH = KH / 2, PW = KW / 2;
   constexpr int HY = kTY + KH - 1, HX = kTX + KW - 1, NPIX = HY * HX;
@@ -116,14 +118,16 @@ __global__ __launch_bounds__(kThreads, 2) void conv_s32_kernel(ConvArgs a) {
   constexpr int MT = kTY / WM;            // 32-pixel row tiles per wave
   constexpr int NT = BN / WN / 32;        // 32-channel column tiles per wave
   static_assert(WM * WN == 4 && MT >= 1 && NT >= 1, "bad wave grid");
+  // T == 1 (1x1 convs): the input tile changes every K-step, so A is staged like B (double buffered in LDS).
+  constexpr bool ADB = (T == 1);
   constexpr int A_BYTES = NPIX * 128, B_BYTES = BN * 128;
-  constexpr int MAIN_BYTES = A_BYTES + 2 * B_BYTES;
+  constexpr int MAIN_BYTES = (ADB ? 2 : 1) * A_BYTES + 2 * B_BYTES;
   constexpr int TS = BN + 4;              // epilogue tile row stride (floats)
   constexpr int EPI_BYTES = kBM * TS * 4;
   constexpr int LDS_BYTES = MAIN_BYTES > EPI_BYTES ? MAIN_BYTES : EPI_BYTES;
   __shared__ __attribute__((aligned(16))) uint8_t smem[LDS_BYTES];
   uint8_t* sA = smem;
-  uint8_t* sB = smem + A_BYTES;
+  uint8_t* sB = smem + (ADB ? 2 : 1) * A_BYTES;
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave / WN, wn = wave % WN;
@@ -137,36 +141,49 @@ __global__ __launch_bounds__(kThreads, 2) void conv_s32_kernel(ConvArgs a) {
   const int n0 = blockIdx.y * BN;
   const long long pix0 = (long long)b * a.H * a.W;
 
-  u32x4 ra[APER], rb[BPER];
-  // staging item -> (halo pixel p, 16-B chunk c): source offset (-1: outside the image -> zeros)
-#define OFLOW_LOAD_A(G)                                                                                              \
+  // Software pipeline. B (weights of one (group, tap) step) is register-staged TWO steps ahead in two register sets
+  // (rb0 / rb1, alternating by step parity: the loop is unrolled by two so that every register index is static) and
+  // double buffered in LDS. A (the input halo of one group) is loaded at the group's first tap and written to LDS at
+  // its last (T steps of lead); for 1x1 convs A follows B's two-step scheme.
+  u32x4 ra0[APER], ra1[APER], rb0[BPER], rb1[BPER];
+  // Every global load of the loop is unconditional (no exec branches around it), so that the compiler can count
+  // vmcnt precisely instead of draining the queue: halo pixels outside the image load a clamped in-image pixel and
+  // are zeroed when written to LDS (the in/out mask and the per-item offsets do not depend on the group).
+  long long aoff[APER];
+  unsigned aok = 0u;
+#pragma unroll
+  for (int s_ = 0; s_ < APER; ++s_) {
+    const int item = (AITEMS % kThreads == 0) ? tid + s_ * kThreads : min(tid + s_ * kThreads, AITEMS - 1);
+    const int p = item >> 3, c = item & 7;
+    const int gy = ty0 - PH + p / HX, gx = tx0 - PW + p % HX;
+    const bool ok = static_cast<unsigned>(gy) < static_cast<unsigned>(a.H) && static_cast<unsigned>(gx) < static_cast<unsigned>(a.W);
+    const int cy = min(max(gy, 0), a.H - 1), cx = min(max(gx, 0), a.W - 1);
+    aoff[s_] = (pix0 + (long long)cy * a.W + cx) * a.xps + c * 16;
+    aok |= (ok ? 1u : 0u) << s_;
+  }
+#define OFLOW_LOAD_A(RA, G)                                                                                          \
+  _Pragma("unroll") for (int s_ = 0; s_ < APER; ++s_)                                                                \
+    RA[s_] = *reinterpret_cast<const u32x4*>(a.x + aoff[s_] + (long long)(G) * 128);
+#define OFLOW_WRITE_A(RA, BUF)                                                                                       \
   _Pragma("unroll") for (int s_ = 0; s_ < APER; ++s_) {                                                              \
     const int item = tid + s_ * kThreads;                                                                            \
     const int p = item >> 3, c = item & 7;                                                                           \
-    const int gy = ty0 - PH + p / HX, gx = tx0 - PW + p % HX;                                                        \
-    const bool ok = (AITEMS % kThreads == 0 || item < AITEMS) && static_cast<unsigned>(gy) < static_cast<unsigned>(a.H) && \
-                    static_cast<unsigned>(gx) < static_cast<unsigned>(a.W);                                          \
-    ra[s_] = ok ? *reinterpret_cast<const u32x4*>(a.x + (pix0 + (long long)gy * a.W + gx) * a.xps + (G) * 128 + c * 16) \
-                : u32x4{0u, 0u, 0u, 0u};                                                                             \
+    if (AITEMS % kThreads == 0 || item < AITEMS)                                                                     \
+      *reinterpret_cast<u32x4*>(sA + (BUF) * A_BYTES + p * 128 + ((c ^ swz(p)) << 4)) =                              \
+          ((aok >> s_) & 1u) ? RA[s_] : u32x4{0u, 0u, 0u, 0u};                                                       \
   }
-#define OFLOW_WRITE_A()                                                                                              \
-  _Pragma("unroll") for (int s_ = 0; s_ < APER; ++s_) {                                                              \
-    const int item = tid + s_ * kThreads;                                                                            \
-    const int p = item >> 3, c = item & 7;                                                                           \
-    if (AITEMS % kThreads == 0 || item < AITEMS) *reinterpret_cast<u32x4*>(sA + p * 128 + ((c ^ swz(p)) << 4)) = ra[s_]; \
-  }
-#define OFLOW_LOAD_B(STEP)                                                                                           \
+#define OFLOW_LOAD_B(RB, STEP)                                                                                       \
   _Pragma("unroll") for (int s_ = 0; s_ < BPER; ++s_) {                                                              \
     const int item = tid + s_ * kThreads;                                                                            \
     if (BITEMS % kThreads == 0 || item < BITEMS)                                                                     \
-      rb[s_] = *reinterpret_cast<const u32x4*>(a.w + ((long long)(STEP) * a.npad + n0) * 128 + item * 16);           \
+      RB[s_] = *reinterpret_cast<const u32x4*>(a.w + ((long long)(STEP) * a.npad + n0) * 128 + item * 16);           \
   }
-#define OFLOW_WRITE_B(BUF)                                                                                           \
+#define OFLOW_WRITE_B(RB, BUF)                                                                                       \
   _Pragma("unroll") for (int s_ = 0; s_ < BPER; ++s_) {                                                              \
     const int item = tid + s_ * kThreads;                                                                            \
     const int n = item >> 3, c = item & 7;                                                                           \
     if (BITEMS % kThreads == 0 || item < BITEMS)                                                                     \
-      *reinterpret_cast<u32x4*>(sB + (BUF) * B_BYTES + n * 128 + ((c ^ swz(n)) << 4)) = rb[s_];                      \
+      *reinterpret_cast<u32x4*>(sB + (BUF) * B_BYTES + n * 128 + ((c ^ swz(n)) << 4)) = RB[s_];                      \
   }
 
   f32x16 acc[MT][NT];
@@ -178,56 +195,81 @@ __global__ __launch_bounds__(kThreads, 2) void conv_s32_kernel(ConvArgs a) {
       for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
 
   const int S = a.kg * T;
-  OFLOW_LOAD_A(0);
-  OFLOW_LOAD_B(0);
-  OFLOW_WRITE_A();
-  OFLOW_WRITE_B(0);
+  OFLOW_LOAD_A(ra0, 0);
+  OFLOW_LOAD_B(rb0, 0);
+  OFLOW_WRITE_A(ra0, 0);
+  OFLOW_WRITE_B(rb0, 0);
+  if (S > 1) {
+    OFLOW_LOAD_B(rb1, 1);
+    if constexpr (ADB) { OFLOW_LOAD_A(ra1, 1); }
+  }
   __syncthreads();
 
-  for (int i = 0; i < S; ++i) {
-    const int g = i / T, t = i - g * T;
-    const bool nextB = i + 1 < S;
-    const bool nextA = (t == T - 1) && (g + 1 < a.kg);
-    if (nextB) { OFLOW_LOAD_B(i + 1); }
-    if (nextA) { OFLOW_LOAD_A(g + 1); }
-
-    const int ky = t / KW, kx = t - ky * KW;
-    const uint8_t* bufB = sB + (i & 1) * B_BYTES;
-#pragma unroll
-    for (int s = 0; s < 2; ++s) {
-      half8 ahi[MT], alo[MT], bhi[NT], blo[NT];
-      const int chi = 2 * s + hh, clo = 4 + 2 * s + hh;
-#pragma unroll
-      for (int mt = 0; mt < MT; ++mt) {
-        const int p = (wm * MT + mt + ky) * HX + r + kx;
-        const uint8_t* row = sA + p * 128;
-        ahi[mt] = *reinterpret_cast<const half8*>(row + ((chi ^ swz(p)) << 4));
-        alo[mt] = *reinterpret_cast<const half8*>(row + ((clo ^ swz(p)) << 4));
-      }
-#pragma unroll
-      for (int nt = 0; nt < NT; ++nt) {
-        const int n = wn * (BN / WN) + nt * 32 + r;
-        const uint8_t* row = bufB + n * 128;
-        bhi[nt] = *reinterpret_cast<const half8*>(row + ((chi ^ swz(n)) << 4));
-        blo[nt] = *reinterpret_cast<const half8*>(row + ((clo ^ swz(n)) << 4));
-      }
-#pragma unroll
-      for (int mt = 0; mt < MT; ++mt)
-#pragma unroll
-        for (int nt = 0; nt < NT; ++nt) {
-          acc[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ahi[mt], blo[nt], acc[mt][nt], 0, 0, 0);
-          acc[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(alo[mt], bhi[nt], acc[mt][nt], 0, 0, 0);
-          acc[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ahi[mt], bhi[nt], acc[mt][nt], 0, 0, 0);
-        }
-    }
-
-    if (nextA) {
-      __syncthreads();  // every wave is done with A(g)
-      OFLOW_WRITE_A();
-    }
-    if (nextB) { OFLOW_WRITE_B((i + 1) & 1); }
-    __syncthreads();
+#define OFLOW_MFMA_BLOCK(S_)                                                                                         \
+  {                                                                                                                  \
+    if constexpr ((VAR & 1) != 0) __builtin_amdgcn_s_setprio(1);                                                     \
+    _Pragma("unroll") for (int mt = 0; mt < MT; ++mt)                                                                \
+      _Pragma("unroll") for (int nt = 0; nt < NT; ++nt) {                                                            \
+        acc[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ahi[S_][mt], blo[S_][nt], acc[mt][nt], 0, 0, 0);        \
+        acc[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(alo[S_][mt], bhi[S_][nt], acc[mt][nt], 0, 0, 0);        \
+        acc[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ahi[S_][mt], bhi[S_][nt], acc[mt][nt], 0, 0, 0);        \
+      }                                                                                                              \
+    if constexpr ((VAR & 1) != 0) __builtin_amdgcn_s_setprio(0);                                                     \
   }
+
+  // one K-step: B(i) is in LDS buffer i&1, the register set RBN holds B(i+1), RBF is free (its B(i) is in LDS)
+#define OFLOW_STEP(I, RAF, RAN, RBF, RBN)                                                                            \
+  {                                                                                                                  \
+    const int i_ = (I);                                                                                              \
+    const int g = i_ / T, t = i_ - g * T;                                                                            \
+    {                                                                                                                \
+      const int i2 = i_ + 2 < S ? i_ + 2 : S - 1; /* past the end: a harmless re-load */                           \
+      OFLOW_LOAD_B(RBF, i2);                                                                                         \
+      if constexpr (ADB) { OFLOW_LOAD_A(RAF, i2); }                                                                  \
+    }                                                                                                                \
+    if constexpr (!ADB) {                                                                                            \
+      if (t == 0) { OFLOW_LOAD_A(ra0, g + 1 < a.kg ? g + 1 : g); }                                                   \
+    }                                                                                                                \
+    const int ky = t / KW, kx = t - ky * KW;                                                                         \
+    const uint8_t* bufA = sA + (ADB ? (i_ & 1) * A_BYTES : 0);                                                       \
+    const uint8_t* bufB = sB + (i_ & 1) * B_BYTES;                                                                   \
+    half8 ahi[2][MT], alo[2][MT], bhi[2][NT], blo[2][NT];                                                          \
+    _Pragma("unroll") for (int s = 0; s < 2; ++s) {                                                                  \
+      const int chi = 2 * s + hh, clo = 4 + 2 * s + hh;                                                              \
+      _Pragma("unroll") for (int mt = 0; mt < MT; ++mt) {                                                            \
+        const int p = (wm * MT + mt + ky) * HX + r + kx;                                                             \
+        const uint8_t* row = bufA + p * 128;                                                                         \
+        ahi[s][mt] = *reinterpret_cast<const half8*>(row + ((chi ^ swz(p)) << 4));                                   \
+        alo[s][mt] = *reinterpret_cast<const half8*>(row + ((clo ^ swz(p)) << 4));                                   \
+      }                                                                                                              \
+      _Pragma("unroll") for (int nt = 0; nt < NT; ++nt) {                                                            \
+        const int n = wn * (BN / WN) + nt * 32 + r;                                                                  \
+        const uint8_t* row = bufB + n * 128;                                                                         \
+        bhi[s][nt] = *reinterpret_cast<const half8*>(row + ((chi ^ swz(n)) << 4));                                   \
+        blo[s][nt] = *reinterpret_cast<const half8*>(row + ((clo ^ swz(n)) << 4));                                   \
+      }                                                                                                              \
+      if constexpr (!(VAR & 2)) { OFLOW_MFMA_BLOCK(s); }                                                             \
+    }                                                                                                                \
+    if constexpr ((VAR & 2) != 0) { OFLOW_MFMA_BLOCK(0); OFLOW_MFMA_BLOCK(1); }                                      \
+    if constexpr (!ADB) {                                                                                            \
+      if (t == T - 1 && g + 1 < a.kg) {                                                                              \
+        __syncthreads(); /* every wave is done with A(g) */                                                          \
+        OFLOW_WRITE_A(ra0, 0);                                                                                       \
+      }                                                                                                              \
+    }                                                                                                                \
+    if (i_ + 1 < S) {                                                                                                \
+      OFLOW_WRITE_B(RBN, (i_ + 1) & 1);                                                                              \
+      if constexpr (ADB) { OFLOW_WRITE_A(RAN, (i_ + 1) & 1); }                                                       \
+    }                                                                                                                \
+    __syncthreads();                                                                                                 \
+  }
+
+  for (int i = 0; i < S; i += 2) {
+    OFLOW_STEP(i, ra0, ra1, rb0, rb1);
+    if (i + 1 < S) OFLOW_STEP(i + 1, ra1, ra0, rb1, rb0);
+  }
+#undef OFLOW_STEP
+#undef OFLOW_MFMA_BLOCK
 
 #undef OFLOW_LOAD_A
 #undef OFLOW_WRITE_A
@@ -269,34 +311,62 @@ __global__ __launch_bounds__(kThreads, 2) void conv_s32_kernel(ConvArgs a) {
     }
   }
   if constexpr (EPI == 0) {
-    if (a.stats != nullptr && tid < BN) {
-      // per-tile instance-norm partials of the conv output (Chan et al. merge in oflow_norm_stats_finalize)
-      const int n = n0 + tid;
-      if (n < a.N) {
-        const float ws = a.wsc[n], bi = a.bias ? a.bias[n] : 0.f;
-        int cnt = 0;
-        float sum = 0.f;
-        for (int pl = 0; pl < kBM; ++pl) {
+    if (a.stats != nullptr) {
+      // per-tile instance-norm partials of the conv output (merged by oflow_norm_stats_finalize): SL = 256 / BN
+      // adjacent lanes share a channel and take interleaved slices of the tile's pixels (two-pass mean / M2 in
+      // fp32); the slices are merged across those lanes with xor shuffles (Chan et al.).
+      constexpr int SL = kThreads / BN >= 4 ? 4 : kThreads / BN >= 2 ? 2 : 1;
+      const int c = tid / SL, sl = tid % SL;
+      const int n = n0 + c;
+      const bool on = c < BN && n < a.N;
+      const float ws = on ? a.wsc[n] : 0.f, bi = (on && a.bias) ? a.bias[n] : 0.f;
+      int cnt = 0;
+      float sum = 0.f;
+      if (on) {
+        for (int pl = sl; pl < kBM; pl += SL) {
           const int y = ty0 + pl / kTX, x = tx0 + (pl % kTX);
           if (y < a.H && x < a.W) {
-            sum += sT[pl * TS + tid] * ws + bi;
+            sum += sT[pl * TS + c] * ws + bi;
             ++cnt;
           }
         }
-        const float mean = sum / static_cast<float>(cnt);
-        float m2 = 0.f;
-        for (int pl = 0; pl < kBM; ++pl) {
+      }
+      float N0 = static_cast<float>(cnt), M0 = cnt ? sum / N0 : 0.f, Q0 = 0.f;
+      if (on) {
+        for (int pl = sl; pl < kBM; pl += SL) {
           const int y = ty0 + pl / kTX, x = tx0 + (pl % kTX);
           if (y < a.H && x < a.W) {
-            const float d = sT[pl * TS + tid] * ws + bi - mean;
-            m2 += d * d;
+            const float d = sT[pl * TS + c] * ws + bi - M0;
+            Q0 += d * d;
           }
         }
+      }
+#pragma unroll
+      for (int m = 1; m < SL; m <<= 1) {
+        const float nb = __shfl_xor(N0, m), mb = __shfl_xor(M0, m), qb = __shfl_xor(Q0, m);
+        const float nn = N0 + nb;
+        if (nb > 0.f) {
+          // symmetric form: both lanes of a pair compute the identical merged value
+          const float lo_n = (sl & m) ? nb : N0, hi_n = (sl & m) ? N0 : nb;
+          const float lo_m = (sl & m) ? mb : M0, hi_m = (sl & m) ? M0 : mb;
+          const float lo_q = (sl & m) ? qb : Q0, hi_q = (sl & m) ? Q0 : qb;
+          if (lo_n > 0.f) {
+            const float d = hi_m - lo_m;
+            M0 = lo_m + d * (hi_n / nn);
+            Q0 = lo_q + hi_q + d * d * (lo_n * hi_n / nn);
+          } else {
+            M0 = hi_m;
+            Q0 = hi_q;
+          }
+          N0 = nn;
+        }
+      }
+      if (on && sl == 0) {
         const int tile_in_img = (ty0 / kTY) * a.tiles_x + tx0 / kTX;
         float* st = a.stats + (((long long)b * a.tiles_x * a.tiles_y + tile_in_img) * a.npad + n) * 3;
-        st[0] = static_cast<float>(cnt);
-        st[1] = mean;
-        st[2] = m2;
+        st[0] = N0;
+        st[1] = M0;
+        st[2] = Q0;
       }
     }
     if (a.y0 == nullptr && a.fn == nullptr) return;
@@ -383,37 +453,58 @@ __global__ __launch_bounds__(kThreads, 2) void conv_s32_kernel(ConvArgs a) {
   }
 }
 
-template <int KH, int KW, int BN, int WM, int WN, int EPI>
+template <int KH, int KW, int BN, int WM, int WN, int EPI, int VAR>
 int launch_conv(const ConvArgs& a, hipStream_t s) {
   dim3 grid(a.tiles_x * a.tiles_y * a.B, a.npad / BN);
-  hipLaunchKernelGGL((conv_s32_kernel<KH, KW, BN, WM, WN, EPI>), grid, dim3(kThreads), 0, s, a);
+  hipLaunchKernelGGL((conv_s32_kernel<KH, KW, BN, WM, WN, EPI, VAR>), grid, dim3(kThreads), 0, s, a);
   return launch_status();
 }
 
-template <int KH, int KW, int EPI>
+template <int KH, int KW, int EPI, int VAR>
 int launch_bn(const ConvArgs& a, int bn, hipStream_t s) {
   switch (bn) {
-    case 128: return launch_conv<KH, KW, 128, 2, 2, EPI>(a, s);
-    case 96: return launch_conv<KH, KW, 96, 4, 1, EPI>(a, s);
-    case 64: return launch_conv<KH, KW, 64, 2, 2, EPI>(a, s);
-    case 32: return launch_conv<KH, KW, 32, 4, 1, EPI>(a, s);
+    case 128: return launch_conv<KH, KW, 128, 2, 2, EPI, VAR>(a, s);
+    case 96: return launch_conv<KH, KW, 96, 4, 1, EPI, VAR>(a, s);
+    case 64: return launch_conv<KH, KW, 64, 2, 2, EPI, VAR>(a, s);
+    case 32: return launch_conv<KH, KW, 32, 4, 1, EPI, VAR>(a, s);
     default: return OFLOW_E_SHAPE;
   }
 }
 
-}  // namespace
-}  // namespace oflow
+template <int VAR>
+int dispatch_conv(const ConvArgs& a, int kh, int kw, int block_n, int epilogue, hipStream_t s) {
+  const int key = kh * 16 + kw;
+  switch (epilogue) {
+    case 0:
+      switch (key) {
+        case 0x11: return launch_bn<1, 1, 0, VAR>(a, block_n, s);
+        case 0x22: return launch_bn<2, 2, 0, VAR>(a, block_n, s);
+        case 0x33: return launch_bn<3, 3, 0, VAR>(a, block_n, s);
+        case 0x15: return launch_bn<1, 5, 0, VAR>(a, block_n, s);
+        case 0x51: return launch_bn<5, 1, 0, VAR>(a, block_n, s);
+        default: return OFLOW_E_SHAPE;
+      }
+    case 1:
+      if (block_n != 128) return OFLOW_E_SHAPE;
+      if (key == 0x15) return launch_conv<1, 5, 128, 2, 2, 1, VAR>(a, s);
+      if (key == 0x51) return launch_conv<5, 1, 128, 2, 2, 1, VAR>(a, s);
+      return OFLOW_E_SHAPE;
+    default:
+      if (block_n != 128) return OFLOW_E_SHAPE;
+      if (key == 0x15) return launch_conv<1, 5, 128, 2, 2, 2, VAR>(a, s);
+      if (key == 0x51) return launch_conv<5, 1, 128, 2, 2, 2, VAR>(a, s);
+      return OFLOW_E_SHAPE;
+  }
+}
 
-using namespace oflow;
-
-extern "C" int oflow_conv_s32_ex(const void* d_x, long long x_pixel_stride, int in_groups, const void* d_wpack,
-                                 int n_pad, const float* d_wscale, const float* d_bias, int N, int B, int H, int W, int kh,
-                                 int kw, int block_n, int epilogue, int activation, float out_scale, void* d_y0,
-                                 long long y0_pixel_stride, void* d_y1, long long y1_pixel_stride, float* d_f32,
-                                 long long f32_batch_stride, long long f32_channel_stride, int f32_accumulate,
-                                 float* d_gru_h, float* d_gru_z, int gru_channels, float* d_nhwc, int nhwc_pixel_stride,
-                                 float* d_stats, const void* d_res, long long res_pixel_stride, int res_activation,
-                                 int s2d, void* stream) {
+// argument checks + ConvArgs for oflow_conv_s32_ex (shared with the tools/exp variant harness)
+int build_conv_args(ConvArgs& a, const void* d_x, long long x_pixel_stride, int in_groups, const void* d_wpack,
+                    int n_pad, const float* d_wscale, const float* d_bias, int N, int B, int H, int W, int kh, int kw,
+                    int block_n, int epilogue, int activation, float out_scale, void* d_y0, long long y0_pixel_stride,
+                    void* d_y1, long long y1_pixel_stride, float* d_f32, long long f32_batch_stride,
+                    long long f32_channel_stride, int f32_accumulate, float* d_gru_h, float* d_gru_z, int gru_channels,
+                    float* d_nhwc, int nhwc_pixel_stride, float* d_stats, const void* d_res, long long res_pixel_stride,
+                    int res_activation, int s2d) {
   if (!d_x || !d_wpack || !d_wscale) return OFLOW_E_NULL;
   if (B <= 0 || H <= 0 || W <= 0 || N <= 0 || in_groups <= 0 || n_pad < N || n_pad % block_n) return OFLOW_E_SHAPE;
   if (activation < 0 || activation > 3 || res_activation < 0 || res_activation > 3 || epilogue < 0 || epilogue > 2)
@@ -430,7 +521,7 @@ extern "C" int oflow_conv_s32_ex(const void* d_x, long long x_pixel_stride, int 
       (d_y1 && ((y1_pixel_stride & 127) || ((uintptr_t)d_y1 & 15))) ||
       (d_res && ((res_pixel_stride & 127) || ((uintptr_t)d_res & 15))))
     return OFLOW_E_ALIGN;
-  ConvArgs a{};
+  a = ConvArgs{};
   a.x = static_cast<const uint8_t*>(d_x);
   a.xps = x_pixel_stride;
   a.kg = in_groups;
@@ -464,29 +555,33 @@ extern "C" int oflow_conv_s32_ex(const void* d_x, long long x_pixel_stride, int 
   a.resps = res_pixel_stride;
   a.res_act = res_activation;
   a.s2d = s2d;
-  hipStream_t s = static_cast<hipStream_t>(stream);
-  const int key = kh * 16 + kw;
-  switch (epilogue) {
-    case 0:
-      switch (key) {
-        case 0x11: return launch_bn<1, 1, 0>(a, block_n, s);
-        case 0x22: return launch_bn<2, 2, 0>(a, block_n, s);
-        case 0x33: return launch_bn<3, 3, 0>(a, block_n, s);
-        case 0x15: return launch_bn<1, 5, 0>(a, block_n, s);
-        case 0x51: return launch_bn<5, 1, 0>(a, block_n, s);
-        default: return OFLOW_E_SHAPE;
-      }
-    case 1:
-      if (block_n != 128) return OFLOW_E_SHAPE;
-      if (key == 0x15) return launch_conv<1, 5, 128, 2, 2, 1>(a, s);
-      if (key == 0x51) return launch_conv<5, 1, 128, 2, 2, 1>(a, s);
-      return OFLOW_E_SHAPE;
-    default:
-      if (block_n != 128) return OFLOW_E_SHAPE;
-      if (key == 0x15) return launch_conv<1, 5, 128, 2, 2, 2>(a, s);
-      if (key == 0x51) return launch_conv<5, 1, 128, 2, 2, 2>(a, s);
-      return OFLOW_E_SHAPE;
-  }
+  (void)kh;
+  (void)kw;
+  (void)block_n;
+  return OFLOW_OK;
+}
+
+}  // namespace
+}  // namespace oflow
+
+using namespace oflow;
+
+extern "C" int oflow_conv_s32_ex(const void* d_x, long long x_pixel_stride, int in_groups, const void* d_wpack,
+                                 int n_pad, const float* d_wscale, const float* d_bias, int N, int B, int H, int W, int kh,
+                                 int kw, int block_n, int epilogue, int activation, float out_scale, void* d_y0,
+                                 long long y0_pixel_stride, void* d_y1, long long y1_pixel_stride, float* d_f32,
+                                 long long f32_batch_stride, long long f32_channel_stride, int f32_accumulate,
+                                 float* d_gru_h, float* d_gru_z, int gru_channels, float* d_nhwc, int nhwc_pixel_stride,
+                                 float* d_stats, const void* d_res, long long res_pixel_stride, int res_activation,
+                                 int s2d, void* stream) {
+  ConvArgs a;
+  const int st = build_conv_args(a, d_x, x_pixel_stride, in_groups, d_wpack, n_pad, d_wscale, d_bias, N, B, H, W, kh, kw,
+                                 block_n, epilogue, activation, out_scale, d_y0, y0_pixel_stride, d_y1, y1_pixel_stride,
+                                 d_f32, f32_batch_stride, f32_channel_stride, f32_accumulate, d_gru_h, d_gru_z,
+                                 gru_channels, d_nhwc, nhwc_pixel_stride, d_stats, d_res, res_pixel_stride,
+                                 res_activation, s2d);
+  if (st != OFLOW_OK) return st;
+  return dispatch_conv<0>(a, kh, kw, block_n, epilogue, static_cast<hipStream_t>(stream));
 }
 
 extern "C" int oflow_conv_s32(const void* d_x, long long x_pixel_stride, int in_groups, const void* d_wpack, int n_pad,
