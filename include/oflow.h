@@ -18,6 +18,7 @@
  *   oflow_grid_warp_f32     <- optical_flow/operator/operator.py:8-56 (warp, warp_grid -> F.grid_sample)
  *   oflow_conv_s32 & co.    <- methods/raft/model/update.py:40-161 (update-block convolutions)
  *   oflow_stem_patches_s32, oflow_norm_*, oflow_conv_s32_ex <- methods/raft/model/extractor.py:35-231 (encoders)
+ *   oflow_convex_upsample_f32 <- methods/raft/model/raft.py:73-85 (RAFT.upsample_flow)
  */
 #ifndef OFLOW_H_
 #define OFLOW_H_
@@ -214,6 +215,14 @@ int oflow_norm_apply_s32(const float* d_x, int C, int B, int H, int W, const flo
                          int activation, int res_mode, const void* d_res, long long res_pixel_stride, const float* d_x2,
                          const float* d_alpha2, const float* d_beta2, int res_activation, int s2d, void* d_y,
                          long long y_pixel_stride, void* stream);
+
+/*
+ * Convex upsampling (methods/raft/model/raft.py:73-85, RAFT.upsample_flow; csrc/upsample.hip).
+ * oflow_convex_upsample_f32: flow (B, 2, H, W), mask (B, 576, H, W) (the mask head output, already x0.25) ->
+ *   out (B, 2, 8H, 8W): softmax over the 9 neighbours of each 8x8 sub-pixel, convex combination of 8*flow over the
+ *   zero-padded 3x3 neighbourhood. B, H <= 65535.
+ */
+int oflow_convex_upsample_f32(const float* d_flow, const float* d_mask, int B, int H, int W, float* d_out, void* stream);
 
 #ifdef __cplusplus
 }

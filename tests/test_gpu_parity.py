@@ -227,6 +227,25 @@ def test_warp_matches_oracle_sintel_frame(mode, pad, ac):
         assert err.max().item() <= 2e-2 and err.mean().item() <= 1e-4
 
 
+@pytest.mark.parametrize("width", [331, 332])
+@pytest.mark.parametrize("sigma", [0.0, 2.0, 40.0, 300.0])
+@pytest.mark.parametrize("pad", ["zeros", "border", "reflection"])
+def test_warp_bilinear_staged_and_direct_tiles(sigma, pad, width):
+    """The bilinear warp stages a tile's source box in LDS when its taps fit (small sigma) and gathers directly
+    otherwise (sigma 300 px; single far-out pixels inside otherwise staged tiles; rows that are not 16-B multiples,
+    width 331): both against the oracle."""
+    img0, _ = synthetic.synthetic_pair(2, 150, width, seed=5)
+    px = torch.from_numpy(synthetic.hash_normal(12, (2, 2, 150, width), sigma))
+    px[0, :, 7, 5] = torch.tensor([5000.0, -3000.0])  # one pixel far outside the frame
+    for ac in (False, True):
+        flow = oop.normalize(px)
+        ref = oop.warp(img0, flow, "bilinear", pad, ac)
+        got = optical_flow.warp(img0.to(DEV), flow.to(DEV), "bilinear", pad, ac).cpu()
+        err = (got - ref).abs()
+        # as test_warp_matches_oracle_sintel_frame: ulp-level grid differences times the frame gradient
+        assert err.max().item() <= 2e-2 and err.mean().item() <= 1e-4, (sigma, pad, ac, err.max().item())
+
+
 def test_grid_sample_and_bilinear_sampler_match_oracle():
     img = torch.from_numpy(synthetic.hash_normal(8, (6, 3, 20, 30), 1.0))
     coords = torch.from_numpy(synthetic.hash_normal(9, (6, 7, 5, 2), 12.0)) + 12.0

@@ -170,3 +170,18 @@ def test_split_encoder_matches_module(norm, b, h, w):
     print(f"{norm} {b}x{h}x{w}: max |d| {err:.2e} (max |ref| {scale:.2f})")
     assert got.shape == ref.shape
     assert err <= 1e-4 * max(1.0, scale), err
+
+
+@pytest.mark.parametrize("shape", [(2, 55, 128), (1, 1, 1), (3, 7, 33), (1, 47, 156)])
+def test_convex_upsample_matches_oracle(shape):
+    """RAFT.upsample_flow on the GPU (one fused kernel, csrc/upsample.hip) vs the reference formula (raft.py:73-85) on
+    the CPU: softmax over the 9 neighbours, unfold with zero padding at every border, permute/reshape order."""
+    b, h, w = shape
+    flow = torch.from_numpy(synthetic.hash_normal(21, (b, 2, h, w), 6.0))
+    mask = torch.from_numpy(synthetic.hash_normal(22, (b, 576, h, w), 3.0))
+    ref = oraft.upsample_flow(flow, mask)
+    with torch.inference_mode():
+        got = RAFT.upsample_flow(flow.to(DEV), mask.to(DEV)).cpu()
+    assert got.shape == ref.shape == (b, 2, 8 * h, 8 * w)
+    tol = 1e-5 * float(8 * flow.abs().max()) + 1e-6
+    assert float((got - ref).abs().max()) <= tol

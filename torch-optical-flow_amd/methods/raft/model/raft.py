@@ -28,6 +28,8 @@ import torch.nn as nn
 import torch.nn.functional as F
 from torch import Tensor
 
+from optical_flow import _native
+
 from .corr import AlternateCorrBlock, CorrBlock
 from .extractor import BasicEncoder, SplitEncoder
 from .update import BasicUpdateBlock, FusedUpdate, SplitUpdate
@@ -125,6 +127,8 @@ class RAFT(nn.Module):
     @staticmethod
     def upsample_flow(flow: Tensor, mask: Tensor) -> Tensor:
         """[H/8, W/8, 2] -> [H, W, 2] by a softmax-weighted 3x3 convex combination (`raft.py:73-85`)."""
+        if flow.is_cuda and not (torch.is_grad_enabled() and (flow.requires_grad or mask.requires_grad)):
+            return _native.convex_upsample(flow, mask)  # one fused HIP kernel (csrc/upsample.hip)
         n, _, h, w = flow.shape
         mask = torch.softmax(mask.view(n, 1, 9, 8, 8, h, w), dim=2)
         up_flow = F.unfold(8 * flow, [3, 3], padding=1).view(n, 2, 9, 1, 1, h, w)

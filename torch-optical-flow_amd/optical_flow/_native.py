@@ -52,6 +52,7 @@ SYMBOLS = (
     "oflow_stem_patches_s32",
     "oflow_norm_stats_finalize",
     "oflow_norm_apply_s32",
+    "oflow_convex_upsample_f32",
 )
 
 _lib = None
@@ -160,6 +161,8 @@ def load() -> ctypes.CDLL:
     lib.oflow_corr_lookup_tiled_s32.argtypes = [PP, IP, IP, I, P, I, I, I, I, P, L, P]
     lib.oflow_corr_lookup_otf_f16.restype = I
     lib.oflow_corr_lookup_otf_f16.argtypes = [P, PP, IP, IP, I, P, I, I, I, I, I, P, P]
+    lib.oflow_convex_upsample_f32.restype = I
+    lib.oflow_convex_upsample_f32.argtypes = [P, P, I, I, I, P, P]
     v = lib.oflow_abi_version()
     if v != ABI_VERSION:
         raise RuntimeError(f"liboflow_hip.so ABI version {v}, expected {ABI_VERSION}: rebuild the library")
@@ -379,6 +382,25 @@ def grid_warp(frame: torch.Tensor, flow: torch.Tensor, mode: str, padding_mode: 
             ),
             what,
         )
+    return out
+
+
+def convex_upsample(flow: torch.Tensor, mask: torch.Tensor) -> torch.Tensor:
+    """RAFT.upsample_flow (methods/raft/model/raft.py:73-85): flow (B, 2, H, W), mask (B, 576, H, W) ->
+    (B, 2, 8H, 8W), one fused kernel (softmax over 9 neighbours x unfold(8 * flow) x sum x permute)."""
+    what = "upsample_flow"
+    fl = _gpu_f32(flow, "flow", what)
+    mk = _gpu_f32(mask, "mask", what)
+    if fl.dim() != 4 or fl.shape[1] != 2 or mk.dim() != 4 or mk.shape[1] != 576 or mk.shape[0] != fl.shape[0] or mk.shape[2:] != fl.shape[2:]:
+        raise RuntimeError(f"{what}: flow {tuple(flow.shape)} must be (B, 2, H, W) and mask {tuple(mask.shape)} (B, 576, H, W)")
+    if fl.device != mk.device:
+        raise RuntimeError(f"{what}: flow and mask are on different devices")
+    b, _, h, w = fl.shape
+    out = torch.empty((b, 2, 8 * h, 8 * w), device=fl.device, dtype=torch.float32)
+    if out.numel() == 0:
+        return out
+    with torch.cuda.device(fl.device), _Timed("upsample_flow", fl.device):
+        _check(load().oflow_convex_upsample_f32(fl.data_ptr(), mk.data_ptr(), b, h, w, out.data_ptr(), _stream(fl.device)), what)
     return out
 
 
