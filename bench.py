@@ -249,7 +249,8 @@ def main() -> int:
                 tr = json.load(f).get(f"{args.workload}:{ppg}")
             traffic = tr.get("hbm_bytes_per_launch") if tr else None
         line["roofline"] = {
-            "kernel": "corr_lookup",
+            "kernel": "corr_lookup" + ("_tiled_s32 (RAFT forward: lookup written as convc1's split-fp16 input)"
+                                       if args.workload != "corr" and args.update_impl == "split" else ""),
             "bound": "hbm",
             "achieved": round(ach, 1),
             "peak": HBM_PEAK_GBS,
