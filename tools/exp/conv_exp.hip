@@ -19,12 +19,8 @@ extern "C" int exp_conv_s32_var(int var, const void* d_x, long long x_pixel_stri
   hipStream_t s = static_cast<hipStream_t>(stream);
   switch (var) {
     case 0: return oflow::dispatch_conv<0>(a, kh, kw, block_n, epilogue, s);
-    case 1: return oflow::dispatch_conv<1>(a, kh, kw, block_n, epilogue, s);
-    case 2: return oflow::dispatch_conv<2>(a, kh, kw, block_n, epilogue, s);
-    case 3: return oflow::dispatch_conv<3>(a, kh, kw, block_n, epilogue, s);
-    case 4: return oflow::dispatch_conv<4>(a, kh, kw, block_n, epilogue, s);
-    case 6: return oflow::dispatch_conv<6>(a, kh, kw, block_n, epilogue, s);
-    case 7: return oflow::dispatch_conv<7>(a, kh, kw, block_n, epilogue, s);
+    case 1040: return oflow::dispatch_conv<1040>(a, kh, kw, block_n, epilogue, s);
+    case 1072: return oflow::dispatch_conv<1072>(a, kh, kw, block_n, epilogue, s);
     default: return OFLOW_E_MODE;
   }
 }

@@ -88,7 +88,7 @@ def main():
             N.conv_s32(N.S32Slice(x), cw, bn, **kw_)
             torch.cuda.synchronize()
             outs[v] = (y.clone(), kw_)
-        eq = {v: bool(torch.equal(outs[v][0], outs[VARS[0]][0])) for v in VARS}
+        eq = {v: bool(torch.equal(outs[v][0], outs[VARS[0]][0])) for v in VARS}  # ablations (VAR >= 128) differ
         times = {v: [] for v in VARS}
         for _ in range(5):
             for v in VARS:
@@ -97,18 +97,28 @@ def main():
                 times[v].append(timed(lambda: N.conv_s32(N.S32Slice(x), cw, bn, **kw_), 20) * 1e3)
         res[name] = {str(v): (round(statistics.median(t), 1), round(min(t), 1), eq[v]) for v, t in times.items()}
         print(name, res[name], flush=True)
-    # encoder layer1 shape (fnet: 16 images at 220x512, 64 -> 64 3x3, instance-norm epilogue: raw fp32 NHWC + stats)
+    # encoder layer1 shape (fnet: 16 images at 220x512, 64 -> 64 3x3): epilogue ablation at VAR 0
     bb, hh, ww = 16, 220, 512
     x = s32(2, bb, hh, ww)
     cw = weights(64, 64, 3, 3, 64)
     raw = torch.empty((bb * hh * ww, 64), device=dev)
     part = torch.empty((bb, N.conv_tiles(hh, ww), 64, 3), device=dev)
-    times = {v: [] for v in VARS}
+    ys = N.s32_empty(bb, hh, ww, 2, dev)
+    cases = {
+        "nhwc+stats": dict(nhwc=raw, stats=part),
+        "nhwc": dict(nhwc=raw),
+        "stats": dict(stats=part),
+        "s32": dict(y0=N.S32Slice(ys)),
+    }
+    times = {(k, v): [] for k in cases for v in VARS}
     for _ in range(3):
-        for v in VARS:
-            Proxy.var = v
-            times[v].append(timed(lambda: N.conv_s32(N.S32Slice(x), cw, 64, nhwc=raw, stats=part), 5) * 1e3)
-    res["enc l1 3x3 64 inorm"] = {str(v): round(statistics.median(t), 1) for v, t in times.items()}
+        for k, kw_ in cases.items():
+            for v in VARS:
+                Proxy.var = v
+                times[(k, v)].append(timed(lambda: N.conv_s32(N.S32Slice(x), cw, 64, **kw_), 5) * 1e3)
+    res["enc l1 3x3 64 epilogues"] = {f"{k}/{v}": round(statistics.median(t), 1) for (k, v), t in times.items()}
+    # and the same conv at BN 64 with 32-px-wide tiles vs a 3x3 128 -> 128 (layer-3-like) shape
+    print(res["enc l1 3x3 64 epilogues"], flush=True)
     print(json.dumps(res))
 
 

@@ -31,7 +31,7 @@ typedef _Float16 half8 __attribute__((ext_vector_type(8)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));  // native vector: stays in VGPRs (HIP uint4 is copied by memcpy)
 
-constexpr int kTY = 4, kTX = 32, kBM = kTY * kTX, kThreads = 256;
+constexpr int kTY = 4, kTX = 32, kThreads = 256;  // default tile: kTY rows x kTX columns
 
 __device__ __forceinline__ int swz(int row) { return (row >> 1) & 7; }
 
@@ -107,23 +107,33 @@ __device__ __forceinline__ void store_s32(uint8_t* y, long long ps, long long P,
 }
 
 // VAR (experiment hooks, 0 in the product): bit 0 s_setprio(1) around each MFMA block; bit 1 issue both K-halves'
-// LDS operand reads before the MFMAs; bit 2 ask for 3 waves per SIMD.
-template <int KH, int KW, int BN, int WM, int WN, int EPI, int VAR = 0>
+// LDS operand reads before the MFMAs; bit 2 ask for 3 waves per SIMD; bit 3 (launcher) 8-row tiles for BN 64;
+// bits 4-6 see BREG / PADL / launch_128. Ablations (wrong results, timing only): bit 7 no global loads in the loop,
+// bit 9 no per-step barrier.
+// BREG: the weight fragments go straight from global memory (L2) into registers, one step of lead, instead of
+// through LDS: no weight slab in LDS and no per-step barrier (A changes once per group); waves as 1 x 4.
+template <int KH, int KW, int BN, int WM, int WN, int EPI, int VAR = 0, int TY = kTY, bool BREG = false>
 __global__ __launch_bounds__(kThreads, (VAR & 4) ? 3 : 2) void conv_s32_kernel(ConvArgs a) {
   constexpr int T = KH * KW;
+  constexpr int BM = TY * kTX;  // output pixels per workgroup (TY rows x 32 columns)
   constexpr int PH = KH / 2, PW = KW / 2;
-  constexpr int HY = kTY + KH - 1, HX = kTX + KW - 1, NPIX = HY * HX;
+  constexpr int HY = TY + KH - 1, HX = kTX + KW - 1, NPIX = HY * HX;
   constexpr int AITEMS = NPIX * 8, APER = (AITEMS + kThreads - 1) / kThreads;
   constexpr int BITEMS = BN * 8, BPER = (BITEMS + kThreads - 1) / kThreads;
-  constexpr int MT = kTY / WM;            // 32-pixel row tiles per wave
+  constexpr int MT = TY / WM;            // 32-pixel row tiles per wave
   constexpr int NT = BN / WN / 32;        // 32-channel column tiles per wave
   static_assert(WM * WN == 4 && MT >= 1 && NT >= 1, "bad wave grid");
   // T == 1 (1x1 convs): the input tile changes every K-step, so A is staged like B (double buffered in LDS).
   constexpr bool ADB = (T == 1);
-  constexpr int A_BYTES = NPIX * 128, B_BYTES = BN * 128;
-  constexpr int MAIN_BYTES = (ADB ? 2 : 1) * A_BYTES + 2 * B_BYTES;
+  // LDS row format: PADL (VAR bit 5) = 144-B rows (128 B + 16 B pad: rows r and r+1 start 9 slots apart, so any 16
+  // consecutive rows of a ds_read_b128 cover distinct bank groups) with affine addressing; else 128-B rows with the
+  // 16-B slot XOR swizzle (slot ^= (row >> 1) & 7), whose per-lane address math is redone every step.
+  constexpr bool PADL = (VAR & 32) != 0;
+  constexpr int RS = PADL ? 144 : 128;
+  constexpr int A_BYTES = NPIX * RS, B_BYTES = BN * RS;
+  constexpr int MAIN_BYTES = (ADB ? 2 : 1) * A_BYTES + (BREG ? 0 : 2 * B_BYTES);
   constexpr int TS = BN + 4;              // epilogue tile row stride (floats)
-  constexpr int EPI_BYTES = kBM * TS * 4;
+  constexpr int EPI_BYTES = BM * TS * 4;
   constexpr int LDS_BYTES = MAIN_BYTES > EPI_BYTES ? MAIN_BYTES : EPI_BYTES;
   __shared__ __attribute__((aligned(16))) uint8_t smem[LDS_BYTES];
   uint8_t* sA = smem;
@@ -136,7 +146,7 @@ __global__ __launch_bounds__(kThreads, (VAR & 4) ? 3 : 2) void conv_s32_kernel(C
   int tile = blockIdx.x;
   const int tx0 = (tile % a.tiles_x) * kTX;
   tile /= a.tiles_x;
-  const int ty0 = (tile % a.tiles_y) * kTY;
+  const int ty0 = (tile % a.tiles_y) * TY;
   const int b = tile / a.tiles_y;
   const int n0 = blockIdx.y * BN;
   const long long pix0 = (long long)b * a.H * a.W;
@@ -169,7 +179,7 @@ __global__ __launch_bounds__(kThreads, (VAR & 4) ? 3 : 2) void conv_s32_kernel(C
     const int item = tid + s_ * kThreads;                                                                            \
     const int p = item >> 3, c = item & 7;                                                                           \
     if (AITEMS % kThreads == 0 || item < AITEMS)                                                                     \
-      *reinterpret_cast<u32x4*>(sA + (BUF) * A_BYTES + p * 128 + ((c ^ swz(p)) << 4)) =                              \
+      *reinterpret_cast<u32x4*>(sA + (BUF) * A_BYTES + p * RS + ((PADL ? c : (c ^ swz(p))) << 4)) =                 \
           ((aok >> s_) & 1u) ? RA[s_] : u32x4{0u, 0u, 0u, 0u};                                                       \
   }
 #define OFLOW_LOAD_B(RB, STEP)                                                                                       \
@@ -183,7 +193,7 @@ __global__ __launch_bounds__(kThreads, (VAR & 4) ? 3 : 2) void conv_s32_kernel(C
     const int item = tid + s_ * kThreads;                                                                            \
     const int n = item >> 3, c = item & 7;                                                                           \
     if (BITEMS % kThreads == 0 || item < BITEMS)                                                                     \
-      *reinterpret_cast<u32x4*>(sB + (BUF) * B_BYTES + n * 128 + ((c ^ swz(n)) << 4)) = RB[s_];                      \
+      *reinterpret_cast<u32x4*>(sB + (BUF) * B_BYTES + n * RS + ((PADL ? c : (c ^ swz(n))) << 4)) = RB[s_];         \
   }
 
   f32x16 acc[MT][NT];
@@ -195,12 +205,26 @@ __global__ __launch_bounds__(kThreads, (VAR & 4) ? 3 : 2) void conv_s32_kernel(C
       for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
 
   const int S = a.kg * T;
+  // BREG fragment sets: [sub-step][nt], set 0 = even steps, set 1 = odd steps
+  half8 f0h[2][NT], f0l[2][NT], f1h[2][NT], f1l[2][NT];
+#define OFLOW_LOAD_F(FH, FL, STEP)                                                                                   \
+  _Pragma("unroll") for (int s_ = 0; s_ < 2; ++s_)                                                                   \
+    _Pragma("unroll") for (int nt_ = 0; nt_ < NT; ++nt_) {                                                           \
+      const uint8_t* row_ = a.w + ((long long)(STEP) * a.npad + n0 + wn * (BN / WN) + nt_ * 32 + r) * 128;          \
+      FH[s_][nt_] = *reinterpret_cast<const half8*>(row_ + (2 * s_ + hh) * 16);                                      \
+      FL[s_][nt_] = *reinterpret_cast<const half8*>(row_ + (4 + 2 * s_ + hh) * 16);                                  \
+    }
   OFLOW_LOAD_A(ra0, 0);
-  OFLOW_LOAD_B(rb0, 0);
+  if constexpr (BREG) {
+    OFLOW_LOAD_F(f0h, f0l, 0);
+    OFLOW_LOAD_F(f1h, f1l, S > 1 ? 1 : 0);
+  } else {
+    OFLOW_LOAD_B(rb0, 0);
+  }
   OFLOW_WRITE_A(ra0, 0);
-  OFLOW_WRITE_B(rb0, 0);
+  if constexpr (!BREG) { OFLOW_WRITE_B(rb0, 0); }
   if (S > 1) {
-    OFLOW_LOAD_B(rb1, 1);
+    if constexpr (!BREG) { OFLOW_LOAD_B(rb1, 1); }
     if constexpr (ADB) { OFLOW_LOAD_A(ra1, 1); }
   }
   __syncthreads();
@@ -218,17 +242,17 @@ __global__ __launch_bounds__(kThreads, (VAR & 4) ? 3 : 2) void conv_s32_kernel(C
   }
 
   // one K-step: B(i) is in LDS buffer i&1, the register set RBN holds B(i+1), RBF is free (its B(i) is in LDS)
-#define OFLOW_STEP(I, RAF, RAN, RBF, RBN)                                                                            \
+#define OFLOW_STEP(I, RAF, RAN, RBF, RBN, FH, FL)                                                                    \
   {                                                                                                                  \
     const int i_ = (I);                                                                                              \
     const int g = i_ / T, t = i_ - g * T;                                                                            \
     {                                                                                                                \
       const int i2 = i_ + 2 < S ? i_ + 2 : S - 1; /* past the end: a harmless re-load */                           \
-      OFLOW_LOAD_B(RBF, i2);                                                                                         \
-      if constexpr (ADB) { OFLOW_LOAD_A(RAF, i2); }                                                                  \
+      if constexpr (!BREG && !(VAR & 128)) { OFLOW_LOAD_B(RBF, i2); }                                                \
+      if constexpr (ADB && !(VAR & 128)) { OFLOW_LOAD_A(RAF, i2); }                                                  \
     }                                                                                                                \
     if constexpr (!ADB) {                                                                                            \
-      if (t == 0) { OFLOW_LOAD_A(ra0, g + 1 < a.kg ? g + 1 : g); }                                                   \
+      if (t == 0 && !(VAR & 128)) { OFLOW_LOAD_A(ra0, g + 1 < a.kg ? g + 1 : g); }                                   \
     }                                                                                                                \
     const int ky = t / KW, kx = t - ky * KW;                                                                         \
     const uint8_t* bufA = sA + (ADB ? (i_ & 1) * A_BYTES : 0);                                                       \
@@ -238,35 +262,96 @@ __global__ __launch_bounds__(kThreads, (VAR & 4) ? 3 : 2) void conv_s32_kernel(C
       const int chi = 2 * s + hh, clo = 4 + 2 * s + hh;                                                              \
       _Pragma("unroll") for (int mt = 0; mt < MT; ++mt) {                                                            \
         const int p = (wm * MT + mt + ky) * HX + r + kx;                                                             \
-        const uint8_t* row = bufA + p * 128;                                                                         \
-        ahi[s][mt] = *reinterpret_cast<const half8*>(row + ((chi ^ swz(p)) << 4));                                   \
-        alo[s][mt] = *reinterpret_cast<const half8*>(row + ((clo ^ swz(p)) << 4));                                   \
+        const uint8_t* row = bufA + p * RS;                                                                          \
+        ahi[s][mt] = *reinterpret_cast<const half8*>(row + ((PADL ? chi : (chi ^ swz(p))) << 4));                    \
+        alo[s][mt] = *reinterpret_cast<const half8*>(row + ((PADL ? clo : (clo ^ swz(p))) << 4));                    \
       }                                                                                                              \
       _Pragma("unroll") for (int nt = 0; nt < NT; ++nt) {                                                            \
-        const int n = wn * (BN / WN) + nt * 32 + r;                                                                  \
-        const uint8_t* row = bufB + n * 128;                                                                         \
-        bhi[s][nt] = *reinterpret_cast<const half8*>(row + ((chi ^ swz(n)) << 4));                                   \
-        blo[s][nt] = *reinterpret_cast<const half8*>(row + ((clo ^ swz(n)) << 4));                                   \
+        if constexpr (BREG) {                                                                                        \
+          bhi[s][nt] = FH[s][nt];                                                                                    \
+          blo[s][nt] = FL[s][nt];                                                                                    \
+        } else {                                                                                                     \
+          const int n = wn * (BN / WN) + nt * 32 + r;                                                                \
+          const uint8_t* row = bufB + n * RS;                                                                        \
+          bhi[s][nt] = *reinterpret_cast<const half8*>(row + ((PADL ? chi : (chi ^ swz(n))) << 4));                  \
+          blo[s][nt] = *reinterpret_cast<const half8*>(row + ((PADL ? clo : (clo ^ swz(n))) << 4));                  \
+        }                                                                                                            \
       }                                                                                                              \
       if constexpr (!(VAR & 2)) { OFLOW_MFMA_BLOCK(s); }                                                             \
     }                                                                                                                \
     if constexpr ((VAR & 2) != 0) { OFLOW_MFMA_BLOCK(0); OFLOW_MFMA_BLOCK(1); }                                      \
+    if constexpr (BREG) { /* this step's fragment set is consumed: refill it two steps ahead */                    \
+      OFLOW_LOAD_F(FH, FL, i_ + 2 < S ? i_ + 2 : S - 1);                                                             \
+    }                                                                                                                \
     if constexpr (!ADB) {                                                                                            \
       if (t == T - 1 && g + 1 < a.kg) {                                                                              \
         __syncthreads(); /* every wave is done with A(g) */                                                          \
         OFLOW_WRITE_A(ra0, 0);                                                                                       \
+        if constexpr (BREG) __syncthreads(); /* A(g+1) visible to every wave */                                     \
       }                                                                                                              \
     }                                                                                                                \
     if (i_ + 1 < S) {                                                                                                \
-      OFLOW_WRITE_B(RBN, (i_ + 1) & 1);                                                                              \
+      if constexpr (!BREG) { OFLOW_WRITE_B(RBN, (i_ + 1) & 1); }                                                     \
       if constexpr (ADB) { OFLOW_WRITE_A(RAN, (i_ + 1) & 1); }                                                       \
     }                                                                                                                \
-    __syncthreads();                                                                                                 \
+    if constexpr ((!BREG || ADB) && !(VAR & 512)) __syncthreads();                                                   \
   }
 
-  for (int i = 0; i < S; i += 2) {
-    OFLOW_STEP(i, ra0, ra1, rb0, rb1);
-    if (i + 1 < S) OFLOW_STEP(i + 1, ra1, ra0, rb1, rb0);
+  if constexpr (BREG && !ADB && (VAR & 1024) != 0) {
+    // Pipelined register-direct loop (VAR bit 10): the A operands of tap t+1 are read from LDS into the other
+    // register set BEFORE tap t's MFMAs, so the MFMA chain covers the LDS latency; the halo changes (barrier) only at
+    // group boundaries, where the next tap's reads are issued after the new halo is visible.
+    // operand sets per K-half (sub-step): set 0 feeds sub-step 0 of every tap, set 1 sub-step 1
+    half8 p0h[MT], p0l[MT], p1h[MT], p1l[MT];
+#define OFLOW_READ_OPS(XH, XL, J, S_)                                                                                \
+  {                                                                                                                  \
+    const int tj_ = (J) % T, ky_ = tj_ / KW, kx_ = tj_ - ky_ * KW;                                                   \
+    _Pragma("unroll") for (int mt_ = 0; mt_ < MT; ++mt_) {                                                           \
+      const int p_ = (wm * MT + mt_ + ky_) * HX + r + kx_;                                                           \
+      const uint8_t* row_ = sA + p_ * RS;                                                                            \
+      const int ch_ = 2 * (S_) + hh, cl_ = 4 + 2 * (S_) + hh;                                                        \
+      XH[mt_] = *reinterpret_cast<const half8*>(row_ + ((PADL ? ch_ : (ch_ ^ swz(p_))) << 4));                       \
+      XL[mt_] = *reinterpret_cast<const half8*>(row_ + ((PADL ? cl_ : (cl_ ^ swz(p_))) << 4));                       \
+    }                                                                                                                \
+  }
+#define OFLOW_MFMA_SUB(XH, XL, FH, FL, S_)                                                                           \
+  _Pragma("unroll") for (int mt = 0; mt < MT; ++mt)                                                                  \
+    _Pragma("unroll") for (int nt = 0; nt < NT; ++nt) {                                                              \
+      acc[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(XH[mt], FL[S_][nt], acc[mt][nt], 0, 0, 0);                \
+      acc[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(XL[mt], FH[S_][nt], acc[mt][nt], 0, 0, 0);                \
+      acc[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(XH[mt], FH[S_][nt], acc[mt][nt], 0, 0, 0);                \
+    }
+#define OFLOW_PSTEP(I, FH, FL)                                                                                       \
+  {                                                                                                                  \
+    const int i_ = (I);                                                                                              \
+    const int g = i_ / T, t = i_ - g * T;                                                                            \
+    if (t == 0) { OFLOW_LOAD_A(ra0, g + 1 < a.kg ? g + 1 : g); }                                                     \
+    OFLOW_READ_OPS(p1h, p1l, i_, 1); /* sub-step 1 operands in flight during sub-step 0 */                          \
+    OFLOW_MFMA_SUB(p0h, p0l, FH, FL, 0);                                                                             \
+    const bool same_ = t != T - 1 && i_ + 1 < S;                                                                     \
+    if (same_) OFLOW_READ_OPS(p0h, p0l, i_ + 1, 0); /* next tap, same halo */                                       \
+    OFLOW_MFMA_SUB(p1h, p1l, FH, FL, 1);                                                                             \
+    OFLOW_LOAD_F(FH, FL, i_ + 2 < S ? i_ + 2 : S - 1);                                                               \
+    if (t == T - 1 && i_ + 1 < S) {                                                                                  \
+      __syncthreads(); /* every wave is done with A(g) */                                                            \
+      OFLOW_WRITE_A(ra0, 0);                                                                                         \
+      __syncthreads(); /* A(g+1) visible */                                                                          \
+      OFLOW_READ_OPS(p0h, p0l, i_ + 1, 0);                                                                           \
+    }                                                                                                                \
+  }
+    OFLOW_READ_OPS(p0h, p0l, 0, 0);
+    for (int i = 0; i < S; i += 2) {
+      OFLOW_PSTEP(i, f0h, f0l);
+      if (i + 1 < S) OFLOW_PSTEP(i + 1, f1h, f1l);
+    }
+#undef OFLOW_PSTEP
+#undef OFLOW_MFMA_SUB
+#undef OFLOW_READ_OPS
+  } else {
+    for (int i = 0; i < S; i += 2) {
+      OFLOW_STEP(i, ra0, ra1, rb0, rb1, f0h, f0l);
+      if (i + 1 < S) OFLOW_STEP(i + 1, ra1, ra0, rb1, rb0, f1h, f1l);
+    }
   }
 #undef OFLOW_STEP
 #undef OFLOW_MFMA_BLOCK
@@ -275,8 +360,17 @@ __global__ __launch_bounds__(kThreads, (VAR & 4) ? 3 : 2) void conv_s32_kernel(C
 #undef OFLOW_WRITE_A
 #undef OFLOW_LOAD_B
 #undef OFLOW_WRITE_B
+#undef OFLOW_LOAD_F
 
+  if constexpr ((VAR & 256) != 0) {  // ablation: no epilogue (accumulators kept live)
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt) asm volatile("" ::"v"(acc[mt][nt]));
+    return;
+  }
   // ---- epilogue: accumulators -> LDS tile [pixel][channel] ----
+  if constexpr (BREG && !ADB) __syncthreads();  // every wave is done reading A before the tile overwrites it
   float* sT = reinterpret_cast<float*>(smem);
 #pragma unroll
   for (int mt = 0; mt < MT; ++mt)
@@ -294,8 +388,8 @@ __global__ __launch_bounds__(kThreads, (VAR & 4) ? 3 : 2) void conv_s32_kernel(C
 
   if (a.f != nullptr) {
     // fp32 NCHW: lanes = consecutive pixels of one tile row (128-B rows of the destination)
-    for (int item = tid; item < kBM * BN; item += kThreads) {
-      const int nl = item / kBM, pl = item - nl * kBM;
+    for (int item = tid; item < BM * BN; item += kThreads) {
+      const int nl = item / BM, pl = item - nl * BM;
       const int n = n0 + nl;
       const int y = ty0 + pl / kTX, x = tx0 + (pl % kTX);
       if (n < a.N && y < a.H && x < a.W) {
@@ -323,7 +417,7 @@ __global__ __launch_bounds__(kThreads, (VAR & 4) ? 3 : 2) void conv_s32_kernel(C
       int cnt = 0;
       float sum = 0.f;
       if (on) {
-        for (int pl = sl; pl < kBM; pl += SL) {
+        for (int pl = sl; pl < BM; pl += SL) {
           const int y = ty0 + pl / kTX, x = tx0 + (pl % kTX);
           if (y < a.H && x < a.W) {
             sum += sT[pl * TS + c] * ws + bi;
@@ -333,7 +427,7 @@ __global__ __launch_bounds__(kThreads, (VAR & 4) ? 3 : 2) void conv_s32_kernel(C
       }
       float N0 = static_cast<float>(cnt), M0 = cnt ? sum / N0 : 0.f, Q0 = 0.f;
       if (on) {
-        for (int pl = sl; pl < kBM; pl += SL) {
+        for (int pl = sl; pl < BM; pl += SL) {
           const int y = ty0 + pl / kTX, x = tx0 + (pl % kTX);
           if (y < a.H && x < a.W) {
             const float d = sT[pl * TS + c] * ws + bi - M0;
@@ -362,7 +456,7 @@ __global__ __launch_bounds__(kThreads, (VAR & 4) ? 3 : 2) void conv_s32_kernel(C
         }
       }
       if (on && sl == 0) {
-        const int tile_in_img = (ty0 / kTY) * a.tiles_x + tx0 / kTX;
+        const int tile_in_img = (ty0 / TY) * a.tiles_x + tx0 / kTX;
         float* st = a.stats + (((long long)b * a.tiles_x * a.tiles_y + tile_in_img) * a.npad + n) * 3;
         st[0] = N0;
         st[1] = M0;
@@ -374,7 +468,7 @@ __global__ __launch_bounds__(kThreads, (VAR & 4) ? 3 : 2) void conv_s32_kernel(C
 
   // S32 / GRU consumers: one thread = one pixel x 8 consecutive channels
   constexpr int C8 = BN / 8;
-  for (int item = tid; item < kBM * C8; item += kThreads) {
+  for (int item = tid; item < BM * C8; item += kThreads) {
     const int pl = item / C8, c8 = item - pl * C8;
     const int nl = c8 * 8, n = n0 + nl;
     const int y = ty0 + pl / kTX, x = tx0 + (pl % kTX);
@@ -453,19 +547,35 @@ __global__ __launch_bounds__(kThreads, (VAR & 4) ? 3 : 2) void conv_s32_kernel(C
   }
 }
 
-template <int KH, int KW, int BN, int WM, int WN, int EPI, int VAR>
-int launch_conv(const ConvArgs& a, hipStream_t s) {
+template <int KH, int KW, int BN, int WM, int WN, int EPI, int VAR, int TY = kTY, bool BREG = false>
+int launch_conv(const ConvArgs& a0, hipStream_t s) {
+  ConvArgs a = a0;
+  a.tiles_y = (a.H + TY - 1) / TY;
   dim3 grid(a.tiles_x * a.tiles_y * a.B, a.npad / BN);
-  hipLaunchKernelGGL((conv_s32_kernel<KH, KW, BN, WM, WN, EPI, VAR>), grid, dim3(kThreads), 0, s, a);
+  hipLaunchKernelGGL((conv_s32_kernel<KH, KW, BN, WM, WN, EPI, VAR, TY, BREG>), grid, dim3(kThreads), 0, s, a);
   return launch_status();
+}
+
+// BN 128: the LDS-staged weight slab (2 x 2 waves) or, with VAR bit 4 (16), register-direct fragments (1 x 4 waves)
+template <int KH, int KW, int EPI, int VAR>
+int launch_128(const ConvArgs& a, hipStream_t s) {
+  // VAR bit 6 (64): 256-channel workgroups (1 x 4 waves of 128 px x 64 ch, register-direct weights) where N allows
+  if constexpr ((VAR & 64) != 0)
+    if (a.npad % 256 == 0) return launch_conv<KH, KW, 256, 1, 4, EPI, VAR, kTY, true>(a, s);
+  if constexpr ((VAR & 16) != 0) return launch_conv<KH, KW, 128, 1, 4, EPI, VAR, kTY, true>(a, s);
+  return launch_conv<KH, KW, 128, 2, 2, EPI, VAR>(a, s);
 }
 
 template <int KH, int KW, int EPI, int VAR>
 int launch_bn(const ConvArgs& a, int bn, hipStream_t s) {
   switch (bn) {
-    case 128: return launch_conv<KH, KW, 128, 2, 2, EPI, VAR>(a, s);
+    case 128: return launch_128<KH, KW, EPI, VAR>(a, s);
     case 96: return launch_conv<KH, KW, 96, 4, 1, EPI, VAR>(a, s);
-    case 64: return launch_conv<KH, KW, 64, 2, 2, EPI, VAR>(a, s);
+    case 64:
+      // 8-row tiles (each wave 64 px x 64 ch: 8 operand reads per 12 MFMAs instead of 6 per 6): 4-5 % faster
+      // (tools/exp/run_conv_exp.py), except with instance-norm partials, whose layout is 4-row tiles
+      if ((VAR & 8) != 0 || a.stats == nullptr) return launch_conv<KH, KW, 64, 4, 1, EPI, VAR, 8>(a, s);
+      return launch_conv<KH, KW, 64, 2, 2, EPI, VAR>(a, s);
     case 32: return launch_conv<KH, KW, 32, 4, 1, EPI, VAR>(a, s);
     default: return OFLOW_E_SHAPE;
   }
@@ -486,13 +596,13 @@ int dispatch_conv(const ConvArgs& a, int kh, int kw, int block_n, int epilogue, 
       }
     case 1:
       if (block_n != 128) return OFLOW_E_SHAPE;
-      if (key == 0x15) return launch_conv<1, 5, 128, 2, 2, 1, VAR>(a, s);
-      if (key == 0x51) return launch_conv<5, 1, 128, 2, 2, 1, VAR>(a, s);
+      if (key == 0x15) return launch_128<1, 5, 1, VAR>(a, s);
+      if (key == 0x51) return launch_128<5, 1, 1, VAR>(a, s);
       return OFLOW_E_SHAPE;
     default:
       if (block_n != 128) return OFLOW_E_SHAPE;
-      if (key == 0x15) return launch_conv<1, 5, 128, 2, 2, 2, VAR>(a, s);
-      if (key == 0x51) return launch_conv<5, 1, 128, 2, 2, 2, VAR>(a, s);
+      if (key == 0x15) return launch_128<1, 5, 2, VAR>(a, s);
+      if (key == 0x51) return launch_128<5, 1, 2, VAR>(a, s);
       return OFLOW_E_SHAPE;
   }
 }
