@@ -195,6 +195,11 @@ int oflow_corr_lookup_tiled_s32(const float* const* d_levels, const int* level_h
  *                   input form of the next stage's stride-2 convolutions (a 3x3/2 conv = a 2x2/1 conv on s2d input,
  *                   a 1x1/2 conv = a 1x1 conv over the first N channels of it).  kh x kw also allows 2x2 (taps at
  *                   offsets -1, 0), block_n also 96.
+ * oflow_conv_s32_ex2: oflow_conv_s32_ex whose input may instead be the raw fp32 NHWC output [P][in_groups*32] of the
+ *   previous convolution (x_pixel_stride = in_groups*128), normalised and ReLU'd while it is staged:
+ *   x = max(0, raw * d_in_scale[b, c] + d_in_shift[b, c]) ([B][in_groups*32] each; both NULL = S32 input). The
+ *   instance norm + ReLU between a residual block's two 3x3 convs (extractor.py:75-76) then never materialises.
+ *   3x3, epilogue 0, in_groups <= 4 only (else OFLOW_E_MODE).
  * oflow_stem_patches_s32: 7x7/2 pad-3 patch matrix of a (B, C, H, W) fp32 image: S32 (B, ceil(H/2), ceil(W/2),
  *   out_groups) with channel t*C + c (t = ky*7 + kx), zeros past 49*C.
  * oflow_norm_stats_finalize: merge the partials (fp64 sums) -> alpha = 1/sqrt(var + eps), beta = -mean * alpha, [B][C].
@@ -208,6 +213,14 @@ int oflow_conv_s32_ex(const void* d_x, long long x_pixel_stride, int in_groups, 
                       long long f32_channel_stride, int f32_accumulate, float* d_gru_h, float* d_gru_z,
                       int gru_channels, float* d_nhwc, int nhwc_pixel_stride, float* d_stats, const void* d_res,
                       long long res_pixel_stride, int res_activation, int s2d, void* stream);
+int oflow_conv_s32_ex2(const void* d_x, long long x_pixel_stride, int in_groups, const void* d_wpack, int n_pad,
+                       const float* d_wscale, const float* d_bias, int N, int B, int H, int W, int kh, int kw,
+                       int block_n, int epilogue, int activation, float out_scale, void* d_y0, long long y0_pixel_stride,
+                       void* d_y1, long long y1_pixel_stride, float* d_f32, long long f32_batch_stride,
+                       long long f32_channel_stride, int f32_accumulate, float* d_gru_h, float* d_gru_z,
+                       int gru_channels, float* d_nhwc, int nhwc_pixel_stride, float* d_stats, const void* d_res,
+                       long long res_pixel_stride, int res_activation, int s2d, const float* d_in_scale,
+                       const float* d_in_shift, void* stream);
 int oflow_stem_patches_s32(const float* d_img, int B, int C, int H, int W, void* d_out, int out_groups, void* stream);
 int oflow_norm_stats_finalize(const float* d_partials, int B, int tiles, int n_pad, int C, double eps, float* d_alpha,
                               float* d_beta, void* stream);

@@ -203,3 +203,25 @@ def test_lookup_s32_equals_lookup(sigma):
     # the fp32 -> S32 repacking used by the materialised / on-the-fly paths gives the same layout
     out2 = N.pack_lookup_s32(ref, 4, 4, N.s32_empty(b, h, w, 11, DEV, zero=True))
     assert torch.equal(out2, out)
+
+
+@pytest.mark.parametrize("c,n,bn", [(64, 64, 64), (96, 96, 96), (128, 128, 128)])
+def test_conv_normalise_on_load_equals_norm_apply(c, n, bn):
+    """oflow_conv_s32_ex2 with a raw fp32 NHWC input normalised + ReLU'd while staged (NhwcNormIn) equals the
+    two-pass path: norm_apply -> S32 -> conv (extractor.py:75-76 between a block's two convs)."""
+    b, h, w = 2, 37, 70
+    g = torch.Generator().manual_seed(5)
+    raw = (torch.randn(b * h * w, c, generator=g) * 3 + 0.5).to(DEV)
+    alpha = (torch.rand(b, c, generator=g) + 0.5).to(DEV)
+    beta = torch.randn(b, c, generator=g).to(DEV)
+    wt = (torch.randn(n, c, 3, 3, generator=g) * 0.05).to(DEV)
+    cw = N.ConvWeights(wt, torch.randn(n, generator=g).to(DEV) * 0.1, ((n + 31) // 32) * 32)
+    s32 = N.s32_empty(b, h, w, c // 32, DEV)
+    N.norm_apply(raw, (b, c, h, w), alpha, beta, "relu", N.S32Slice(s32))
+    y1 = torch.zeros(b, n, h, w, device=DEV)
+    y2 = torch.zeros(b, n, h, w, device=DEV)
+    N.conv_s32(N.S32Slice(s32), cw, bn, f32=y1)
+    N.conv_s32(N.NhwcNormIn(raw, b, h, w, alpha, beta), cw, bn, f32=y2)
+    torch.cuda.synchronize()
+    err = float((y1 - y2).abs().max())
+    assert err <= 1e-6 * float(y1.abs().max()), err

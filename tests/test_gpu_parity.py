@@ -315,3 +315,17 @@ def test_corrblock_pyramid_attribute_semantics():
     assert torch.all(after[:, :81] == 0) and torch.equal(after[:, 81:], before[:, 81:])
     cb.corr_pyramid = [p * 2 for p in pyr]
     assert torch.equal(cb(coords)[:, 81:], 2 * before[:, 81:])
+
+
+def test_ops_refuse_autograd_inputs():
+    """No backward kernels (SURVEY §8(f) row 3): an input that requires grad must raise, not silently drop the graph;
+    under no_grad the same call runs."""
+    f = torch.randn(1, 8, 16, 16, device=DEV, requires_grad=True)
+    with pytest.raises(RuntimeError, match="requires grad"):
+        CorrBlock(f, f.detach())
+    frame = torch.rand(1, 3, 8, 8, device=DEV, requires_grad=True)
+    flow = torch.zeros(1, 2, 8, 8, device=DEV)
+    with pytest.raises(RuntimeError, match="requires grad"):
+        optical_flow.warp(frame, flow)
+    with torch.no_grad():
+        assert optical_flow.warp(frame, flow).shape == frame.shape

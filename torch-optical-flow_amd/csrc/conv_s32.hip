@@ -32,6 +32,7 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));  // native vector: stays in VGPRs (HIP uint4 is copied by memcpy)
 
 constexpr int kTY = 4, kTX = 32, kThreads = 256;  // default tile: kTY rows x kTX columns
+constexpr int kAinGroups = 4;                      // AIN inputs: up to 128 channels (the encoders' 64 / 96 / 128)
 
 __device__ __forceinline__ int swz(int row) { return (row >> 1) & 7; }
 
@@ -66,6 +67,10 @@ struct ConvArgs {
   long long resps;
   int res_act;
   int s2d;                 // S32 destinations in space-to-depth layout: pixel (y/2, x/2), channel + ((y&1)*2+(x&1))*N
+  // fp32 NHWC input normalised on load (AIN): x = relu(raw * ia[b, c] + ib[b, c]) -- the previous conv's instance
+  // norm + ReLU (extractor.py:75-76) folded into this conv's operand staging; [B][kg*32] each, or null (S32 input)
+  const float* ia;
+  const float* ib;
 };
 
 __device__ __forceinline__ float act_fn(float v, int act) {
@@ -112,7 +117,8 @@ __device__ __forceinline__ void store_s32(uint8_t* y, long long ps, long long P,
 // bit 9 no per-step barrier.
 // BREG: the weight fragments go straight from global memory (L2) into registers, one step of lead, instead of
 // through LDS: no weight slab in LDS and no per-step barrier (A changes once per group); waves as 1 x 4.
-template <int KH, int KW, int BN, int WM, int WN, int EPI, int VAR = 0, int TY = kTY, bool BREG = false>
+// AIN: the input is fp32 NHWC [P][kg*32] normalised + ReLU'd while staged (ConvArgs.ia / .ib), kg <= kAinGroups.
+template <int KH, int KW, int BN, int WM, int WN, int EPI, int VAR = 0, int TY = kTY, bool BREG = false, bool AIN = false>
 __global__ __launch_bounds__(kThreads, (VAR & 4) ? 3 : 2) void conv_s32_kernel(ConvArgs a) {
   constexpr int T = KH * KW;
   constexpr int BM = TY * kTX;  // output pixels per workgroup (TY rows x 32 columns)
@@ -135,7 +141,9 @@ __global__ __launch_bounds__(kThreads, (VAR & 4) ? 3 : 2) void conv_s32_kernel(C
   constexpr int TS = BN + 4;              // epilogue tile row stride (floats)
   constexpr int EPI_BYTES = BM * TS * 4;
   constexpr int LDS_BYTES = MAIN_BYTES > EPI_BYTES ? MAIN_BYTES : EPI_BYTES;
-  __shared__ __attribute__((aligned(16))) uint8_t smem[LDS_BYTES];
+  constexpr int AFF_BYTES = AIN ? kAinGroups * 32 * 8 : 0;  // float2 (scale, shift) per input channel
+  __shared__ __attribute__((aligned(16))) uint8_t smem[LDS_BYTES + AFF_BYTES];
+  float2* sAff = reinterpret_cast<float2*>(smem + LDS_BYTES);
   uint8_t* sA = smem;
   uint8_t* sB = smem + (ADB ? 2 : 1) * A_BYTES;
 
@@ -174,13 +182,34 @@ __global__ __launch_bounds__(kThreads, (VAR & 4) ? 3 : 2) void conv_s32_kernel(C
 #define OFLOW_LOAD_A(RA, G)                                                                                          \
   _Pragma("unroll") for (int s_ = 0; s_ < APER; ++s_)                                                                \
     RA[s_] = *reinterpret_cast<const u32x4*>(a.x + aoff[s_] + (long long)(G) * 128);
-#define OFLOW_WRITE_A(RA, BUF)                                                                                       \
+#define OFLOW_WRITE_A(RA, BUF, G)                                                                                    \
   _Pragma("unroll") for (int s_ = 0; s_ < APER; ++s_) {                                                              \
     const int item = tid + s_ * kThreads;                                                                            \
     const int p = item >> 3, c = item & 7;                                                                           \
-    if (AITEMS % kThreads == 0 || item < AITEMS)                                                                     \
-      *reinterpret_cast<u32x4*>(sA + (BUF) * A_BYTES + p * RS + ((PADL ? c : (c ^ swz(p))) << 4)) =                 \
-          ((aok >> s_) & 1u) ? RA[s_] : u32x4{0u, 0u, 0u, 0u};                                                       \
+    if (AITEMS % kThreads == 0 || item < AITEMS) {                                                                   \
+      if constexpr (AIN) {                                                                                           \
+        /* 4 fp32 channels (G*32 + 4c ..) -> relu(x * scale + shift) -> 4 hi + 4 lo halves (8 B each) */             \
+        typedef _Float16 half4_ __attribute__((ext_vector_type(4)));                                                 \
+        half4_ h4 = {0, 0, 0, 0}, l4 = {0, 0, 0, 0};                                                                 \
+        if ((aok >> s_) & 1u) {                                                                                      \
+          const float* fv = reinterpret_cast<const float*>(&RA[s_]);                                                 \
+          _Pragma("unroll") for (int e_ = 0; e_ < 4; ++e_) {                                                         \
+            const float2 af = sAff[(G) * 32 + 4 * c + e_];                                                           \
+            float v_ = fv[e_] * af.x + af.y;                                                                         \
+            v_ = v_ < 0.f ? 0.f : v_;                                                                                \
+            const _Float16 hv = static_cast<_Float16>(v_);                                                           \
+            h4[e_] = hv;                                                                                             \
+            l4[e_] = static_cast<_Float16>(v_ - static_cast<float>(hv));                                             \
+          }                                                                                                          \
+        }                                                                                                            \
+        uint8_t* rw_ = sA + (BUF) * A_BYTES + p * RS + (c & 1) * 8;                                                  \
+        *reinterpret_cast<half4_*>(rw_ + ((PADL ? (c >> 1) : ((c >> 1) ^ swz(p))) << 4)) = h4;                       \
+        *reinterpret_cast<half4_*>(rw_ + ((PADL ? 4 + (c >> 1) : ((4 + (c >> 1)) ^ swz(p))) << 4)) = l4;             \
+      } else {                                                                                                       \
+        *reinterpret_cast<u32x4*>(sA + (BUF) * A_BYTES + p * RS + ((PADL ? c : (c ^ swz(p))) << 4)) =               \
+            ((aok >> s_) & 1u) ? RA[s_] : u32x4{0u, 0u, 0u, 0u};                                                     \
+      }                                                                                                              \
+    }                                                                                                                \
   }
 #define OFLOW_LOAD_B(RB, STEP)                                                                                       \
   _Pragma("unroll") for (int s_ = 0; s_ < BPER; ++s_) {                                                              \
@@ -214,6 +243,11 @@ __global__ __launch_bounds__(kThreads, (VAR & 4) ? 3 : 2) void conv_s32_kernel(C
       FH[s_][nt_] = *reinterpret_cast<const half8*>(row_ + (2 * s_ + hh) * 16);                                      \
       FL[s_][nt_] = *reinterpret_cast<const half8*>(row_ + (4 + 2 * s_ + hh) * 16);                                  \
     }
+  if constexpr (AIN) {
+    for (int e = tid; e < a.kg * 32; e += kThreads)
+      sAff[e] = make_float2(a.ia[(long long)b * a.kg * 32 + e], a.ib[(long long)b * a.kg * 32 + e]);
+    __syncthreads();
+  }
   OFLOW_LOAD_A(ra0, 0);
   if constexpr (BREG) {
     OFLOW_LOAD_F(f0h, f0l, 0);
@@ -221,7 +255,7 @@ __global__ __launch_bounds__(kThreads, (VAR & 4) ? 3 : 2) void conv_s32_kernel(C
   } else {
     OFLOW_LOAD_B(rb0, 0);
   }
-  OFLOW_WRITE_A(ra0, 0);
+  OFLOW_WRITE_A(ra0, 0, 0);
   if constexpr (!BREG) { OFLOW_WRITE_B(rb0, 0); }
   if (S > 1) {
     if constexpr (!BREG) { OFLOW_LOAD_B(rb1, 1); }
@@ -286,13 +320,13 @@ __global__ __launch_bounds__(kThreads, (VAR & 4) ? 3 : 2) void conv_s32_kernel(C
     if constexpr (!ADB) {                                                                                            \
       if (t == T - 1 && g + 1 < a.kg) {                                                                              \
         __syncthreads(); /* every wave is done with A(g) */                                                          \
-        OFLOW_WRITE_A(ra0, 0);                                                                                       \
+        OFLOW_WRITE_A(ra0, 0, g + 1);                                                                                \
         if constexpr (BREG) __syncthreads(); /* A(g+1) visible to every wave */                                     \
       }                                                                                                              \
     }                                                                                                                \
     if (i_ + 1 < S) {                                                                                                \
       if constexpr (!BREG) { OFLOW_WRITE_B(RBN, (i_ + 1) & 1); }                                                     \
-      if constexpr (ADB) { OFLOW_WRITE_A(RAN, (i_ + 1) & 1); }                                                       \
+      if constexpr (ADB) { OFLOW_WRITE_A(RAN, (i_ + 1) & 1, i_ + 1); }                                               \
     }                                                                                                                \
     if constexpr ((!BREG || ADB) && !(VAR & 512)) __syncthreads();                                                   \
   }
@@ -334,7 +368,7 @@ __global__ __launch_bounds__(kThreads, (VAR & 4) ? 3 : 2) void conv_s32_kernel(C
     OFLOW_LOAD_F(FH, FL, i_ + 2 < S ? i_ + 2 : S - 1);                                                               \
     if (t == T - 1 && i_ + 1 < S) {                                                                                  \
       __syncthreads(); /* every wave is done with A(g) */                                                            \
-      OFLOW_WRITE_A(ra0, 0);                                                                                         \
+      OFLOW_WRITE_A(ra0, 0, g + 1);                                                                                  \
       __syncthreads(); /* A(g+1) visible */                                                                          \
       OFLOW_READ_OPS(p0h, p0l, i_ + 1, 0);                                                                           \
     }                                                                                                                \
@@ -552,6 +586,13 @@ int launch_conv(const ConvArgs& a0, hipStream_t s) {
   ConvArgs a = a0;
   a.tiles_y = (a.H + TY - 1) / TY;
   dim3 grid(a.tiles_x * a.tiles_y * a.B, a.npad / BN);
+  if constexpr (KH == 3 && KW == 3 && EPI == 0 && !BREG) {  // the encoders' second block convs
+    if (a.ia != nullptr) {
+      hipLaunchKernelGGL((conv_s32_kernel<KH, KW, BN, WM, WN, EPI, VAR, TY, BREG, true>), grid, dim3(kThreads), 0, s, a);
+      return launch_status();
+    }
+  }
+  if (a.ia != nullptr) return OFLOW_E_MODE;
   hipLaunchKernelGGL((conv_s32_kernel<KH, KW, BN, WM, WN, EPI, VAR, TY, BREG>), grid, dim3(kThreads), 0, s, a);
   return launch_status();
 }
@@ -676,6 +717,32 @@ int build_conv_args(ConvArgs& a, const void* d_x, long long x_pixel_stride, int 
 
 using namespace oflow;
 
+extern "C" int oflow_conv_s32_ex2(const void* d_x, long long x_pixel_stride, int in_groups, const void* d_wpack,
+                                  int n_pad, const float* d_wscale, const float* d_bias, int N, int B, int H, int W, int kh,
+                                  int kw, int block_n, int epilogue, int activation, float out_scale, void* d_y0,
+                                  long long y0_pixel_stride, void* d_y1, long long y1_pixel_stride, float* d_f32,
+                                  long long f32_batch_stride, long long f32_channel_stride, int f32_accumulate,
+                                  float* d_gru_h, float* d_gru_z, int gru_channels, float* d_nhwc, int nhwc_pixel_stride,
+                                  float* d_stats, const void* d_res, long long res_pixel_stride, int res_activation,
+                                  int s2d, const float* d_in_scale, const float* d_in_shift, void* stream) {
+  ConvArgs a;
+  const int st = build_conv_args(a, d_x, x_pixel_stride, in_groups, d_wpack, n_pad, d_wscale, d_bias, N, B, H, W, kh, kw,
+                                 block_n, epilogue, activation, out_scale, d_y0, y0_pixel_stride, d_y1, y1_pixel_stride,
+                                 d_f32, f32_batch_stride, f32_channel_stride, f32_accumulate, d_gru_h, d_gru_z,
+                                 gru_channels, d_nhwc, nhwc_pixel_stride, d_stats, d_res, res_pixel_stride,
+                                 res_activation, s2d);
+  if (st != OFLOW_OK) return st;
+  if ((d_in_scale == nullptr) != (d_in_shift == nullptr)) return OFLOW_E_NULL;
+  if (d_in_scale) {
+    // fp32 NHWC input [P][in_groups*32]: pixel stride = 128 B per group, normalised + ReLU'd on load
+    if (kh != 3 || kw != 3 || epilogue != 0 || in_groups > kAinGroups) return OFLOW_E_MODE;
+    if (x_pixel_stride != (long long)in_groups * 128) return OFLOW_E_SHAPE;
+    a.ia = d_in_scale;
+    a.ib = d_in_shift;
+  }
+  return dispatch_conv<0>(a, kh, kw, block_n, epilogue, static_cast<hipStream_t>(stream));
+}
+
 extern "C" int oflow_conv_s32_ex(const void* d_x, long long x_pixel_stride, int in_groups, const void* d_wpack,
                                  int n_pad, const float* d_wscale, const float* d_bias, int N, int B, int H, int W, int kh,
                                  int kw, int block_n, int epilogue, int activation, float out_scale, void* d_y0,
@@ -684,14 +751,11 @@ extern "C" int oflow_conv_s32_ex(const void* d_x, long long x_pixel_stride, int 
                                  float* d_gru_h, float* d_gru_z, int gru_channels, float* d_nhwc, int nhwc_pixel_stride,
                                  float* d_stats, const void* d_res, long long res_pixel_stride, int res_activation,
                                  int s2d, void* stream) {
-  ConvArgs a;
-  const int st = build_conv_args(a, d_x, x_pixel_stride, in_groups, d_wpack, n_pad, d_wscale, d_bias, N, B, H, W, kh, kw,
-                                 block_n, epilogue, activation, out_scale, d_y0, y0_pixel_stride, d_y1, y1_pixel_stride,
-                                 d_f32, f32_batch_stride, f32_channel_stride, f32_accumulate, d_gru_h, d_gru_z,
-                                 gru_channels, d_nhwc, nhwc_pixel_stride, d_stats, d_res, res_pixel_stride,
-                                 res_activation, s2d);
-  if (st != OFLOW_OK) return st;
-  return dispatch_conv<0>(a, kh, kw, block_n, epilogue, static_cast<hipStream_t>(stream));
+  return oflow_conv_s32_ex2(d_x, x_pixel_stride, in_groups, d_wpack, n_pad, d_wscale, d_bias, N, B, H, W, kh, kw,
+                            block_n, epilogue, activation, out_scale, d_y0, y0_pixel_stride, d_y1, y1_pixel_stride,
+                            d_f32, f32_batch_stride, f32_channel_stride, f32_accumulate, d_gru_h, d_gru_z, gru_channels,
+                            d_nhwc, nhwc_pixel_stride, d_stats, d_res, res_pixel_stride, res_activation, s2d, nullptr,
+                            nullptr, stream);
 }
 
 extern "C" int oflow_conv_s32(const void* d_x, long long x_pixel_stride, int in_groups, const void* d_wpack, int n_pad,

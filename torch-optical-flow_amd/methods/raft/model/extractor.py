@@ -188,29 +188,39 @@ class SplitEncoder:
         b, h, w = shape
         bn = self._bn(cw.n)
         V = _native.S32Slice
+        dev = x.device
         if self.inorm:
-            raw = torch.empty((b * h * w, cw.n), device=x.t.device, dtype=torch.float32)
+            raw = torch.empty((b * h * w, cw.n), device=dev, dtype=torch.float32)
             tiles = _native.conv_tiles(h, w)
-            part = torch.empty((b, tiles, cw.n_pad, 3), device=x.t.device, dtype=torch.float32)
+            part = torch.empty((b, tiles, cw.n_pad, 3), device=dev, dtype=torch.float32)
             _native.conv_s32(x, cw, bn, nhwc=raw, stats=part)
             alpha, beta = _native.norm_stats(part, b, tiles, cw.n_pad, cw.n, 1e-5)
             if raw_only:
                 return raw, alpha, beta
             if out is None:
-                out = _native.s32_empty(b, h // 2 if s2d else h, w // 2 if s2d else w, (cw.n * (4 if s2d else 1) + 31) // 32, x.t.device)
+                out = _native.s32_empty(b, h // 2 if s2d else h, w // 2 if s2d else w, (cw.n * (4 if s2d else 1) + 31) // 32, dev)
             if isinstance(res, tuple):
                 _native.norm_apply(raw, (b, cw.n, h, w), alpha, beta, act, V(out), res_raw=res, res_act="relu", s2d=s2d)
             else:
                 _native.norm_apply(raw, (b, cw.n, h, w), alpha, beta, act, V(out), res=res, res_act="relu" if res is not None else "none", s2d=s2d)
             return out
         if raw_only:
-            out = _native.s32_empty(b, h, w, (cw.n + 31) // 32, x.t.device)
+            out = _native.s32_empty(b, h, w, (cw.n + 31) // 32, dev)
             _native.conv_s32(x, cw, bn, y0=V(out))
             return out
         if out is None:
-            out = _native.s32_empty(b, h // 2 if s2d else h, w // 2 if s2d else w, (cw.n * (4 if s2d else 1) + 31) // 32, x.t.device)
+            out = _native.s32_empty(b, h // 2 if s2d else h, w // 2 if s2d else w, (cw.n * (4 if s2d else 1) + 31) // 32, dev)
         _native.conv_s32(x, cw, bn, act=act, y0=V(out), res=res, res_act="relu" if res is not None else "none", s2d=s2d)
         return out
+
+    def _conv1(self, x, cw, shape):
+        """A residual block's first conv -> relu(norm1(.)) as the second conv's input: with instance norm the raw
+        fp32 output and its statistics (normalised + ReLU'd while the next conv stages it, oflow_conv_s32_ex2); with
+        folded batch norm an S32 tensor."""
+        if self.inorm:
+            raw, alpha, beta = self._conv_norm(x, cw, shape, "relu", raw_only=True)
+            return _native.NhwcNormIn(raw, *shape, alpha, beta)
+        return _native.S32Slice(self._conv_norm(x, cw, shape, "relu"))
 
     def __call__(self, x: Union[Tensor, Sequence[Tensor]]) -> Union[Tensor, Tuple[Tensor, ...]]:
         is_list = isinstance(x, (tuple, list))
@@ -234,15 +244,15 @@ class SplitEncoder:
                 out_s2d = last_of_stage and li + 1 < len(layers)  # the next stage starts with stride-2 convs
                 pre = f"{li}.{bi}."
                 if blk.downsample is None:
-                    t = self._conv_norm(V(cur), self.w[pre + "conv1"], (n, h, w), "relu")
-                    cur = self._conv_norm(V(t), self.w[pre + "conv2"], (n, h, w), "relu", res=V(cur), s2d=out_s2d)
+                    t = self._conv1(V(cur), self.w[pre + "conv1"], (n, h, w))
+                    cur = self._conv_norm(t, self.w[pre + "conv2"], (n, h, w), "relu", res=V(cur), s2d=out_s2d)
                 else:
                     h, w = h // 2, w // 2  # cur is the space-to-depth input at the new resolution
-                    t = self._conv_norm(V(cur), self.w[pre + "conv1"], (n, h, w), "relu")
+                    t = self._conv1(V(cur), self.w[pre + "conv1"], (n, h, w))
                     cin = self.w[pre + "down"].kg
                     d = self._conv_norm(V(cur, 0, cin), self.w[pre + "down"], (n, h, w), "none", raw_only=True)
                     res = d if self.inorm else V(d)
-                    cur = self._conv_norm(V(t), self.w[pre + "conv2"], (n, h, w), "relu", res=res, s2d=out_s2d)
+                    cur = self._conv_norm(t, self.w[pre + "conv2"], (n, h, w), "relu", res=res, s2d=out_s2d)
                 if out_s2d:
                     pass  # cur now holds (n, h/2, w/2, 4C) for the next stage
         head = self.w["head"]

@@ -53,6 +53,7 @@ SYMBOLS = (
     "oflow_norm_stats_finalize",
     "oflow_norm_apply_s32",
     "oflow_convex_upsample_f32",
+    "oflow_conv_s32_ex2",
 )
 
 _lib = None
@@ -161,6 +162,8 @@ def load() -> ctypes.CDLL:
     lib.oflow_corr_lookup_tiled_s32.argtypes = [PP, IP, IP, I, P, I, I, I, I, P, L, P]
     lib.oflow_corr_lookup_otf_f16.restype = I
     lib.oflow_corr_lookup_otf_f16.argtypes = [P, PP, IP, IP, I, P, I, I, I, I, I, P, P]
+    lib.oflow_conv_s32_ex2.restype = I
+    lib.oflow_conv_s32_ex2.argtypes = list(lib.oflow_conv_s32_ex.argtypes[:-1]) + [P, P, P]
     lib.oflow_convex_upsample_f32.restype = I
     lib.oflow_convex_upsample_f32.argtypes = [P, P, I, I, I, P, P]
     v = lib.oflow_abi_version()
@@ -185,6 +188,12 @@ def _gpu_f32(t: torch.Tensor, name: str, what: str) -> torch.Tensor:
     if t.device.type != "cuda":
         raise RuntimeError(
             f"{what}: {name} is on {t.device}; this MI355X build runs only on ROCm GPU tensors (no CPU fallback)"
+        )
+    if t.requires_grad and torch.is_grad_enabled():
+        # the kernels have no backward: fail loudly instead of returning a graph-less tensor
+        raise RuntimeError(
+            f"{what}: {name} requires grad; this build implements the inference path only (no backward kernels): "
+            "run under torch.no_grad() / torch.inference_mode(), or detach the input"
         )
     if t.dtype != torch.float32:
         t = t.float()
@@ -589,6 +598,47 @@ class S32Slice:
         """Byte address of the hi half of channel c of the slice."""
         return self.ptr + (c // 32) * 128 + (c % 32) * 2
 
+    @property
+    def bhw(self):
+        return tuple(int(v) for v in self.t.shape[:3])
+
+    @property
+    def device(self):
+        return self.t.device
+
+
+class NhwcNormIn:
+    """Convolution input given as the previous convolution's raw fp32 NHWC output [B*H*W, C] plus its instance-norm
+    affine (scale, shift: [B, C]); the kernel stages relu(raw * scale + shift) (oflow_conv_s32_ex2), so the normalised
+    activation is never written to HBM."""
+
+    __slots__ = ("raw", "bhw", "scale", "shift")
+
+    def __init__(self, raw: torch.Tensor, b: int, h: int, w: int, scale: torch.Tensor, shift: torch.Tensor):
+        c = raw.shape[1]
+        if raw.dtype != torch.float32 or not raw.is_contiguous() or raw.shape[0] != b * h * w or c % 32:
+            raise RuntimeError("NhwcNormIn: raw must be contiguous fp32 [B*H*W, C], C % 32 == 0")
+        for t in (scale, shift):
+            if t.dtype != torch.float32 or not t.is_contiguous() or t.numel() != b * c:
+                raise RuntimeError("NhwcNormIn: scale / shift must be contiguous fp32 [B, C]")
+        self.raw, self.bhw, self.scale, self.shift = raw, (int(b), int(h), int(w)), scale, shift
+
+    @property
+    def ptr(self) -> int:
+        return self.raw.data_ptr()
+
+    @property
+    def ps(self) -> int:
+        return int(self.raw.shape[1]) * 4
+
+    @property
+    def ng(self) -> int:
+        return int(self.raw.shape[1]) // 32
+
+    @property
+    def device(self):
+        return self.raw.device
+
 
 def s32_empty(b: int, h: int, w: int, groups: int, device, zero: bool = False) -> torch.Tensor:
     f = torch.zeros if zero else torch.empty
@@ -659,17 +709,18 @@ def conv_tiles(h: int, w: int) -> int:
 def conv_s32(x: S32Slice, cw: ConvWeights, block_n: int, act: str = "none", out_scale: float = 1.0, y0=None, y1=None,
              f32=None, f32_accumulate: bool = False, epilogue: int = 0, gru_h=None, gru_z=None, nhwc=None, stats=None,
              res=None, res_act: str = "none", s2d: bool = False) -> None:
-    """Split-fp16 convolution (oflow_conv_s32_ex). x: input slice with cw.kg groups. y0/y1: S32Slice destinations
+    """Split-fp16 convolution (oflow_conv_s32_ex2). x: input S32Slice with cw.kg groups, or NhwcNormIn (3x3 only). y0/y1: S32Slice destinations
     (s2d: space-to-depth layout, half the spatial size). f32: (B, N', H, W) fp32 NCHW destination. nhwc: [P, N]
     fp32 destination. stats: instance-norm partials [B, conv_tiles(H, W), n_pad, 3]. res: S32Slice residual added
     after the activation, then res_act. epilogue 1/2: GRU gates / candidate with gru_h, gru_z ([P, CH] fp32)."""
     what = "conv_s32"
     if x.ng != cw.kg:
         raise RuntimeError(f"{what}: input has {x.ng} groups, weights expect {cw.kg}")
-    b, h, w = (int(v) for v in x.t.shape[:3])
+    b, h, w = x.bhw
+    nin = isinstance(x, NhwcNormIn)
     hw_out = (h // 2, w // 2) if s2d else (h, w)
     for d in (y0, y1):
-        if d is not None and (tuple(d.t.shape[:3]) != (b, *hw_out) or d.t.device != x.t.device):
+        if d is not None and (tuple(d.t.shape[:3]) != (b, *hw_out) or d.t.device != x.device):
             raise RuntimeError(f"{what}: destination shape/device mismatch")
     if res is not None and (tuple(res.t.shape[:3]) != (b, h, w) or res.ng * 32 < cw.n):
         raise RuntimeError(f"{what}: residual shape mismatch")
@@ -692,10 +743,10 @@ def conv_s32(x: S32Slice, cw: ConvWeights, block_n: int, act: str = "none", out_
             if tt is None or tt.dtype != torch.float32 or not tt.is_contiguous() or tt.numel() != b * h * w * gch:
                 raise RuntimeError(f"{what}: GRU state tensors must be contiguous fp32 [P, {gch}]")
         gh, gz = gru_h.data_ptr(), gru_z.data_ptr()
-    dev = x.t.device
+    dev = x.device
     with torch.cuda.device(dev), _Timed(f"conv{cw.kh}x{cw.kw}", dev):
         _check(
-            load().oflow_conv_s32_ex(
+            load().oflow_conv_s32_ex2(
                 x.ptr, x.ps, cw.kg, cw.pack.data_ptr(), cw.n_pad, cw.wscale.data_ptr(),
                 cw.bias.data_ptr() if cw.bias is not None else None, cw.n, b, h, w, cw.kh, cw.kw, int(block_n),
                 int(epilogue), ACT[act], float(out_scale), y0.ptr if y0 is not None else None, y0.ps if y0 is not None else 0,
@@ -704,6 +755,7 @@ def conv_s32(x: S32Slice, cw: ConvWeights, block_n: int, act: str = "none", out_
                 nhwc.data_ptr() if nhwc is not None else None, cw.n,
                 stats.data_ptr() if stats is not None else None,
                 res.ptr if res is not None else None, res.ps if res is not None else 0, ACT[res_act], int(bool(s2d)),
+                x.scale.data_ptr() if nin else None, x.shift.data_ptr() if nin else None,
                 _stream(dev),
             ),
             what,
