@@ -249,7 +249,7 @@ def main() -> int:
                 tr = json.load(f).get(f"{args.workload}:{ppg}")
             traffic = tr.get("hbm_bytes_per_launch") if tr else None
         line["roofline"] = {
-            "kernel": "corr_lookup" + ("_tiled_s32 (RAFT forward: lookup written as convc1's split-fp16 input)"
+            "kernel": "corr_lookup" + ("_tiled_nhwc (RAFT forward: fp32 NHWC rows, convc1's input)"
                                        if args.workload != "corr" and args.update_impl == "split" else ""),
             "bound": "hbm",
             "achieved": round(ach, 1),

@@ -49,6 +49,11 @@ extern "C" {
 #define OFLOW_PAD_BORDER 1
 #define OFLOW_PAD_REFLECTION 2
 
+/* oflow_conv_s32_ex2 input formats */
+#define OFLOW_IN_S32 0
+#define OFLOW_IN_F32_NORM 1
+#define OFLOW_IN_F32 2
+
 int oflow_abi_version(void);
 const char* oflow_status_string(int status);
 
@@ -179,6 +184,13 @@ int oflow_pack_s32_f32(const float* d_x, long long x_batch_stride, int C, int B,
                        float* d_nhwc, int nhwc_pixel_stride, void* stream);
 int oflow_flow_prep_s32(const float* d_coords, int B, int H, int W, void* d_patches, void* d_flow0,
                         long long flow0_pixel_stride, void* d_flow1, long long flow1_pixel_stride, void* stream);
+/* oflow_corr_lookup_tiled_nhwc_f32: the tiled lookup as fp32 NHWC rows [B*H*W][row_floats] for the RAFT forward's convc1
+ * (oflow_conv_s32_ex2, OFLOW_IN_F32): level l at channels [l*LS, l*LS + (2r+1)^2), LS = (2r+1)^2 rounded up to 8, every
+ * other channel of the row written as 0; row_floats >= num_levels*LS, a multiple of 32. Same values as
+ * oflow_corr_lookup_tiled_f32. Replaces corr.py:56-77 + the channel concat feeding update.py:120-121. */
+int oflow_corr_lookup_tiled_nhwc_f32(const float* const* d_levels, const int* level_h, const int* level_w, int num_levels,
+                                     const float* d_coords, int B, int H, int W, int radius, float* d_out, int row_floats,
+                                     void* stream);
 int oflow_corr_lookup_tiled_s32(const float* const* d_levels, const int* level_h, const int* level_w, int num_levels,
                                 const float* d_coords, int B, int H, int W, int radius, void* d_out,
                                 long long out_pixel_stride, void* stream);
@@ -195,11 +207,12 @@ int oflow_corr_lookup_tiled_s32(const float* const* d_levels, const int* level_h
  *                   input form of the next stage's stride-2 convolutions (a 3x3/2 conv = a 2x2/1 conv on s2d input,
  *                   a 1x1/2 conv = a 1x1 conv over the first N channels of it).  kh x kw also allows 2x2 (taps at
  *                   offsets -1, 0), block_n also 96.
- * oflow_conv_s32_ex2: oflow_conv_s32_ex whose input may instead be the raw fp32 NHWC output [P][in_groups*32] of the
- *   previous convolution (x_pixel_stride = in_groups*128), normalised and ReLU'd while it is staged:
- *   x = max(0, raw * d_in_scale[b, c] + d_in_shift[b, c]) ([B][in_groups*32] each; both NULL = S32 input). The
- *   instance norm + ReLU between a residual block's two 3x3 convs (extractor.py:75-76) then never materialises.
- *   3x3, epilogue 0, in_groups <= 4 only (else OFLOW_E_MODE).
+ * oflow_conv_s32_ex2: oflow_conv_s32_ex with an input format: OFLOW_IN_S32 (as _ex); OFLOW_IN_F32_NORM: the raw fp32
+ *   NHWC output [P][in_groups*32] of the previous convolution (x_pixel_stride = in_groups*128), normalised and ReLU'd
+ *   while staged, x = max(0, raw * d_in_scale[b, c] + d_in_shift[b, c]) ([B][in_groups*32] each) -- the instance
+ *   norm + ReLU between a residual block's two 3x3 convs (extractor.py:75-76) never materialises (3x3, epilogue 0,
+ *   in_groups <= 4); OFLOW_IN_F32: a dense fp32 NHWC input split into hi + lo while staged (1x1, epilogue 0,
+ *   block_n 128: convc1 reading oflow_corr_lookup_tiled_nhwc_f32's output).
  * oflow_stem_patches_s32: 7x7/2 pad-3 patch matrix of a (B, C, H, W) fp32 image: S32 (B, ceil(H/2), ceil(W/2),
  *   out_groups) with channel t*C + c (t = ky*7 + kx), zeros past 49*C.
  * oflow_norm_stats_finalize: merge the partials (fp64 sums) -> alpha = 1/sqrt(var + eps), beta = -mean * alpha, [B][C].
@@ -219,8 +232,8 @@ int oflow_conv_s32_ex2(const void* d_x, long long x_pixel_stride, int in_groups,
                        void* d_y1, long long y1_pixel_stride, float* d_f32, long long f32_batch_stride,
                        long long f32_channel_stride, int f32_accumulate, float* d_gru_h, float* d_gru_z,
                        int gru_channels, float* d_nhwc, int nhwc_pixel_stride, float* d_stats, const void* d_res,
-                       long long res_pixel_stride, int res_activation, int s2d, const float* d_in_scale,
-                       const float* d_in_shift, void* stream);
+                       long long res_pixel_stride, int res_activation, int s2d, int in_format,
+                       const float* d_in_scale, const float* d_in_shift, void* stream);
 int oflow_stem_patches_s32(const float* d_img, int B, int C, int H, int W, void* d_out, int out_groups, void* stream);
 int oflow_norm_stats_finalize(const float* d_partials, int B, int tiles, int n_pad, int C, double eps, float* d_alpha,
                               float* d_beta, void* stream);

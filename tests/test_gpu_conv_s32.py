@@ -225,3 +225,42 @@ def test_conv_normalise_on_load_equals_norm_apply(c, n, bn):
     torch.cuda.synchronize()
     err = float((y1 - y2).abs().max())
     assert err <= 1e-6 * float(y1.abs().max()), err
+
+
+@pytest.mark.parametrize("sigma", [0.0, 3.0, 25.0])
+@pytest.mark.parametrize("radius,levels", [(4, 4), (2, 3), (3, 5)])
+def test_lookup_nhwc_equals_lookup(sigma, radius, levels):
+    """oflow_corr_lookup_tiled_nhwc_f32 (the RAFT forward's lookup, query-major workgroups) = the NCHW lookup
+    bit-for-bit in the permuted channel order, zeros in every other channel of the row; ragged last workgroup."""
+    g = torch.Generator().manual_seed(int(sigma) + 7 * radius)
+    b, c, h, w = 2, 256, 33, 37
+    f1 = torch.randn(b, c, h, w, generator=g).to(DEV)
+    f2 = torch.randn(b, c, h, w, generator=g).to(DEV)
+    pyr = N.corr_pyramid_tiled(f1, f2, levels)
+    coords = coords_grid(b, h, w, device=DEV) + torch.randn(b, 2, h, w, generator=g).to(DEV) * sigma
+    ref = N.corr_lookup_tiled(pyr, coords, radius)  # (B, L*K*K, H, W)
+    ls, kk = N.lookup_s32_stride(radius), (2 * radius + 1) ** 2
+    row = ((levels * ls + 31) // 32) * 32
+    out = torch.full((b * h * w, row), 7.0, device=DEV)
+    N.corr_lookup_tiled_nhwc(pyr, coords, radius, out)
+    got = out.view(b, h, w, row)
+    expect = torch.zeros_like(got)
+    for lvl in range(levels):
+        expect[..., lvl * ls : lvl * ls + kk] = ref[:, lvl * kk : (lvl + 1) * kk].permute(0, 2, 3, 1)
+    assert torch.equal(got, expect)
+
+
+def test_conv_f32_input_equals_s32_input():
+    """convc1 reading the fp32 NHWC lookup rows (F32In, split while staged) = reading the same values as S32."""
+    g = torch.Generator().manual_seed(3)
+    b, h, w, c, n = 2, 23, 45, 352, 256
+    x = (torch.randn(b * h * w, c, generator=g) * 4).to(DEV)
+    s32 = N.s32_from_f32(x.view(b, h, w, c).permute(0, 3, 1, 2).contiguous())
+    wt = (torch.randn(n, c, 1, 1, generator=g) * 0.05).to(DEV)
+    cw = N.ConvWeights(wt, torch.randn(n, generator=g).to(DEV) * 0.1, 256)
+    y1 = N.s32_empty(b, h, w, 8, DEV, zero=True)
+    y2 = N.s32_empty(b, h, w, 8, DEV, zero=True)
+    N.conv_s32(N.S32Slice(s32), cw, 128, "relu", y0=N.S32Slice(y1))
+    N.conv_s32(N.F32In(x, b, h, w), cw, 128, "relu", y0=N.S32Slice(y2))
+    torch.cuda.synchronize()
+    assert torch.equal(y1, y2)

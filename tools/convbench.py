@@ -113,10 +113,14 @@ def main():
     dims = tp.dims
     lo = N.s32_empty(b, h, w, 11, dev, zero=True)
     ls = timed(lambda: N.corr_lookup_tiled_s32(tp, coords, 4, lo), args.iters * 3)
+    lf = torch.empty((b * h * w, 352), device=dev)
+    lnh = timed(lambda: N.corr_lookup_tiled_nhwc(tp, coords, 4, lf), args.iters * 3)
     ln = timed(lambda: N.corr_lookup_tiled(tp, coords, 4), args.iters * 3)
     lb = lookup_bytes(b, dims)
     out["lookup_s32_us"] = round(ls * 1e3, 1)
     out["lookup_s32_GBs"] = round(lb / ls / 1e6, 1)
+    out["lookup_nhwc_us"] = round(lnh * 1e3, 1)
+    out["lookup_nhwc_GBs"] = round(lb / lnh / 1e6, 1)
     out["lookup_nchw_us"] = round(ln * 1e3, 1)
     out["lookup_nchw_GBs"] = round(lb / ln / 1e6, 1)
     print(json.dumps(out, indent=1))

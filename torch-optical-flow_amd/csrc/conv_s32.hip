@@ -71,7 +71,10 @@ struct ConvArgs {
   // norm + ReLU (extractor.py:75-76) folded into this conv's operand staging; [B][kg*32] each, or null (S32 input)
   const float* ia;
   const float* ib;
+  int ain;                 // input format: kInS32 / kInF32Norm / kInF32
 };
+// input formats of oflow_conv_s32_ex2
+constexpr int kInS32 = OFLOW_IN_S32, kInF32Norm = OFLOW_IN_F32_NORM, kInF32 = OFLOW_IN_F32;
 
 __device__ __forceinline__ float act_fn(float v, int act) {
   if (act == 1) return v < 0.f ? 0.f : v;  // relu; NaN propagates like ATen
@@ -117,8 +120,9 @@ __device__ __forceinline__ void store_s32(uint8_t* y, long long ps, long long P,
 // bit 9 no per-step barrier.
 // BREG: the weight fragments go straight from global memory (L2) into registers, one step of lead, instead of
 // through LDS: no weight slab in LDS and no per-step barrier (A changes once per group); waves as 1 x 4.
-// AIN: the input is fp32 NHWC [P][kg*32] normalised + ReLU'd while staged (ConvArgs.ia / .ib), kg <= kAinGroups.
-template <int KH, int KW, int BN, int WM, int WN, int EPI, int VAR = 0, int TY = kTY, bool BREG = false, bool AIN = false>
+// AIN: kInF32Norm = fp32 NHWC [P][kg*32] input normalised + ReLU'd while staged (ConvArgs.ia / .ib, kg <= kAinGroups);
+// kInF32 = fp32 NHWC input split into hi + lo while staged (the NHWC corr lookup feeding convc1).
+template <int KH, int KW, int BN, int WM, int WN, int EPI, int VAR = 0, int TY = kTY, bool BREG = false, int AIN = kInS32>
 __global__ __launch_bounds__(kThreads, (VAR & 4) ? 3 : 2) void conv_s32_kernel(ConvArgs a) {
   constexpr int T = KH * KW;
   constexpr int BM = TY * kTX;  // output pixels per workgroup (TY rows x 32 columns)
@@ -141,7 +145,7 @@ __global__ __launch_bounds__(kThreads, (VAR & 4) ? 3 : 2) void conv_s32_kernel(C
   constexpr int TS = BN + 4;              // epilogue tile row stride (floats)
   constexpr int EPI_BYTES = BM * TS * 4;
   constexpr int LDS_BYTES = MAIN_BYTES > EPI_BYTES ? MAIN_BYTES : EPI_BYTES;
-  constexpr int AFF_BYTES = AIN ? kAinGroups * 32 * 8 : 0;  // float2 (scale, shift) per input channel
+  constexpr int AFF_BYTES = AIN == kInF32Norm ? kAinGroups * 32 * 8 : 0;  // float2 (scale, shift) per input channel
   __shared__ __attribute__((aligned(16))) uint8_t smem[LDS_BYTES + AFF_BYTES];
   float2* sAff = reinterpret_cast<float2*>(smem + LDS_BYTES);
   uint8_t* sA = smem;
@@ -187,16 +191,19 @@ __global__ __launch_bounds__(kThreads, (VAR & 4) ? 3 : 2) void conv_s32_kernel(C
     const int item = tid + s_ * kThreads;                                                                            \
     const int p = item >> 3, c = item & 7;                                                                           \
     if (AITEMS % kThreads == 0 || item < AITEMS) {                                                                   \
-      if constexpr (AIN) {                                                                                           \
-        /* 4 fp32 channels (G*32 + 4c ..) -> relu(x * scale + shift) -> 4 hi + 4 lo halves (8 B each) */             \
+      if constexpr (AIN != kInS32) {                                                                                 \
+        /* 4 fp32 channels (G*32 + 4c ..) [-> relu(x * scale + shift)] -> 4 hi + 4 lo halves (8 B each) */           \
         typedef _Float16 half4_ __attribute__((ext_vector_type(4)));                                                 \
         half4_ h4 = {0, 0, 0, 0}, l4 = {0, 0, 0, 0};                                                                 \
         if ((aok >> s_) & 1u) {                                                                                      \
           const float* fv = reinterpret_cast<const float*>(&RA[s_]);                                                 \
           _Pragma("unroll") for (int e_ = 0; e_ < 4; ++e_) {                                                         \
-            const float2 af = sAff[(G) * 32 + 4 * c + e_];                                                           \
-            float v_ = fv[e_] * af.x + af.y;                                                                         \
-            v_ = v_ < 0.f ? 0.f : v_;                                                                                \
+            float v_ = fv[e_];                                                                                       \
+            if constexpr (AIN == kInF32Norm) {                                                                       \
+              const float2 af = sAff[(G) * 32 + 4 * c + e_];                                                         \
+              v_ = v_ * af.x + af.y;                                                                                 \
+              v_ = v_ < 0.f ? 0.f : v_;                                                                              \
+            }                                                                                                        \
             const _Float16 hv = static_cast<_Float16>(v_);                                                           \
             h4[e_] = hv;                                                                                             \
             l4[e_] = static_cast<_Float16>(v_ - static_cast<float>(hv));                                             \
@@ -243,7 +250,7 @@ __global__ __launch_bounds__(kThreads, (VAR & 4) ? 3 : 2) void conv_s32_kernel(C
       FH[s_][nt_] = *reinterpret_cast<const half8*>(row_ + (2 * s_ + hh) * 16);                                      \
       FL[s_][nt_] = *reinterpret_cast<const half8*>(row_ + (4 + 2 * s_ + hh) * 16);                                  \
     }
-  if constexpr (AIN) {
+  if constexpr (AIN == kInF32Norm) {
     for (int e = tid; e < a.kg * 32; e += kThreads)
       sAff[e] = make_float2(a.ia[(long long)b * a.kg * 32 + e], a.ib[(long long)b * a.kg * 32 + e]);
     __syncthreads();
@@ -587,12 +594,19 @@ int launch_conv(const ConvArgs& a0, hipStream_t s) {
   a.tiles_y = (a.H + TY - 1) / TY;
   dim3 grid(a.tiles_x * a.tiles_y * a.B, a.npad / BN);
   if constexpr (KH == 3 && KW == 3 && EPI == 0 && !BREG) {  // the encoders' second block convs
-    if (a.ia != nullptr) {
-      hipLaunchKernelGGL((conv_s32_kernel<KH, KW, BN, WM, WN, EPI, VAR, TY, BREG, true>), grid, dim3(kThreads), 0, s, a);
+    if (a.ain == kInF32Norm) {
+      hipLaunchKernelGGL((conv_s32_kernel<KH, KW, BN, WM, WN, EPI, VAR, TY, BREG, kInF32Norm>), grid, dim3(kThreads), 0, s,
+                         a);
       return launch_status();
     }
   }
-  if (a.ia != nullptr) return OFLOW_E_MODE;
+  if constexpr (KH == 1 && KW == 1 && EPI == 0 && BN == 128 && !BREG) {  // convc1 on the NHWC corr lookup
+    if (a.ain == kInF32) {
+      hipLaunchKernelGGL((conv_s32_kernel<KH, KW, BN, WM, WN, EPI, VAR, TY, BREG, kInF32>), grid, dim3(kThreads), 0, s, a);
+      return launch_status();
+    }
+  }
+  if (a.ain != kInS32) return OFLOW_E_MODE;
   hipLaunchKernelGGL((conv_s32_kernel<KH, KW, BN, WM, WN, EPI, VAR, TY, BREG>), grid, dim3(kThreads), 0, s, a);
   return launch_status();
 }
@@ -724,7 +738,8 @@ extern "C" int oflow_conv_s32_ex2(const void* d_x, long long x_pixel_stride, int
                                   long long f32_batch_stride, long long f32_channel_stride, int f32_accumulate,
                                   float* d_gru_h, float* d_gru_z, int gru_channels, float* d_nhwc, int nhwc_pixel_stride,
                                   float* d_stats, const void* d_res, long long res_pixel_stride, int res_activation,
-                                  int s2d, const float* d_in_scale, const float* d_in_shift, void* stream) {
+                                  int s2d, int in_format, const float* d_in_scale, const float* d_in_shift,
+                                  void* stream) {
   ConvArgs a;
   const int st = build_conv_args(a, d_x, x_pixel_stride, in_groups, d_wpack, n_pad, d_wscale, d_bias, N, B, H, W, kh, kw,
                                  block_n, epilogue, activation, out_scale, d_y0, y0_pixel_stride, d_y1, y1_pixel_stride,
@@ -732,14 +747,17 @@ extern "C" int oflow_conv_s32_ex2(const void* d_x, long long x_pixel_stride, int
                                  gru_channels, d_nhwc, nhwc_pixel_stride, d_stats, d_res, res_pixel_stride,
                                  res_activation, s2d);
   if (st != OFLOW_OK) return st;
-  if ((d_in_scale == nullptr) != (d_in_shift == nullptr)) return OFLOW_E_NULL;
-  if (d_in_scale) {
-    // fp32 NHWC input [P][in_groups*32]: pixel stride = 128 B per group, normalised + ReLU'd on load
+  if (in_format < kInS32 || in_format > kInF32) return OFLOW_E_MODE;
+  if (in_format != kInS32 && x_pixel_stride != (long long)in_groups * 128) return OFLOW_E_SHAPE;  // dense [P][kg*32]
+  if (in_format == kInF32Norm) {  // normalised + ReLU'd on load
+    if (!d_in_scale || !d_in_shift) return OFLOW_E_NULL;
     if (kh != 3 || kw != 3 || epilogue != 0 || in_groups > kAinGroups) return OFLOW_E_MODE;
-    if (x_pixel_stride != (long long)in_groups * 128) return OFLOW_E_SHAPE;
     a.ia = d_in_scale;
     a.ib = d_in_shift;
+  } else if (in_format == kInF32) {
+    if (kh != 1 || kw != 1 || epilogue != 0 || block_n != 128) return OFLOW_E_MODE;
   }
+  a.ain = in_format;
   return dispatch_conv<0>(a, kh, kw, block_n, epilogue, static_cast<hipStream_t>(stream));
 }
 
@@ -754,8 +772,8 @@ extern "C" int oflow_conv_s32_ex(const void* d_x, long long x_pixel_stride, int 
   return oflow_conv_s32_ex2(d_x, x_pixel_stride, in_groups, d_wpack, n_pad, d_wscale, d_bias, N, B, H, W, kh, kw,
                             block_n, epilogue, activation, out_scale, d_y0, y0_pixel_stride, d_y1, y1_pixel_stride,
                             d_f32, f32_batch_stride, f32_channel_stride, f32_accumulate, d_gru_h, d_gru_z, gru_channels,
-                            d_nhwc, nhwc_pixel_stride, d_stats, d_res, res_pixel_stride, res_activation, s2d, nullptr,
-                            nullptr, stream);
+                            d_nhwc, nhwc_pixel_stride, d_stats, d_res, res_pixel_stride, res_activation, s2d, kInS32,
+                            nullptr, nullptr, stream);
 }
 
 extern "C" int oflow_conv_s32(const void* d_x, long long x_pixel_stride, int in_groups, const void* d_wpack, int n_pad,

@@ -184,6 +184,98 @@ __global__ __launch_bounds__(kThreads) void corr_lookup_kernel(LookupArgs a) {
   }
 }
 
+
+// NHWC fp32 form for the RAFT forward (oflow_corr_lookup_tiled_nhwc_f32): row q = [level l at l*LS .. l*LS + K^2,
+// zeros elsewhere] of row_floats fp32 (the permuted channel order convc1's packed weights expect). Query-major
+// workgroups: QB = 64 / nlev queries x all levels, so a workgroup owns QB consecutive output rows = one contiguous
+// region, written with consecutive lanes on consecutive floats (full 128-B lines, pads included).
+template <int R>
+__global__ __launch_bounds__(kThreads) void corr_lookup_nhwc_kernel(LookupArgs a, int QB, int row_floats) {
+  constexpr int PK = 2 * R + 2, K = 2 * R + 1, PS = PK * PK, QS = PS + 1;
+  constexpr int ITEMS = kQ * PS, PER = (ITEMS + kThreads - 1) / kThreads;
+  constexpr int KK = K * K, LS = (KK + 7) / 8 * 8;
+  __shared__ float sP[kQ * QS];
+  __shared__ int sX[kQ], sY[kQ], sHl[kQ], sWl[kQ], sWB[kQ];
+  __shared__ float4 sW[kQ];
+  __shared__ const float* sL[kQ];
+  const int pairs = QB * a.nlev;
+  const int q0 = blockIdx.x * QB;
+  if (threadIdx.x < pairs) {
+    const int pr = threadIdx.x, lvl = pr / QB, q = q0 + pr - lvl * QB;
+    int xs = -(1 << 28), ys = -(1 << 28), hl = 0, wl = 0, wb = 1;
+    float4 w = make_float4(0.f, 0.f, 0.f, 0.f);
+    const float* base = nullptr;
+    if (q < a.total) {
+      const int b = q / a.N, pix = q - b * a.N;
+      const float inv = 1.0f / static_cast<float>(1 << lvl);  // exact power of two (corr.py:68)
+      const float cx = a.coords[(size_t)(2 * b) * a.N + pix] * inv;
+      const float cy = a.coords[(size_t)(2 * b + 1) * a.N + pix] * inv;
+      if (fabsf(cx) < 4194304.0f && fabsf(cy) < 4194304.0f) {
+        const float fx = floorf(cx), fy = floorf(cy);
+        const float wx = cx - fx, wy = cy - fy, ex = 1.0f - wx, ey = 1.0f - wy;
+        xs = static_cast<int>(fx) - R;
+        ys = static_cast<int>(fy) - R;
+        w = make_float4(ey * ex, ey * wx, wy * ex, wy * wx);
+      }
+      // level parameters through a switch: kernel-argument arrays indexed by a lane value would go to scratch
+      hl = a.Hl[0]; wl = a.Wl[0]; wb = a.WB[0]; base = a.lv[0];
+      for (int l = 1; l < OFLOW_MAX_LEVELS; ++l)
+        if (l == lvl) { hl = a.Hl[l]; wl = a.Wl[l]; wb = a.WB[l]; base = a.lv[l]; }
+      base += (size_t)q * ((hl + 3) >> 2) * wb * 32;
+    }
+    sX[pr] = xs;
+    sY[pr] = ys;
+    sW[pr] = w;
+    sHl[pr] = hl;
+    sWl[pr] = wl;
+    sWB[pr] = wb;
+    sL[pr] = base;
+  }
+  __syncthreads();
+  float v[PER];
+#pragma unroll
+  for (int s = 0; s < PER; ++s) {
+    const int item = threadIdx.x + kThreads * s;
+    v[s] = 0.0f;
+    if (item < pairs * PS) {
+      const int pr = item / PS, rem = item - pr * PS;
+      const int row = rem / PK, col = rem - row * PK;
+      const int y = sY[pr] + row, x = sX[pr] + col;
+      if (static_cast<unsigned>(y) < static_cast<unsigned>(sHl[pr]) && static_cast<unsigned>(x) < static_cast<unsigned>(sWl[pr]))
+        v[s] = sL[pr][((y >> 2) * sWB[pr] + (x >> 3)) * 32 + ((y & 3) << 3) + (x & 7)];
+    }
+  }
+#pragma unroll
+  for (int s = 0; s < PER; ++s) {
+    const int item = threadIdx.x + kThreads * s;
+    if (item < pairs * PS) {
+      const int pr = item / PS;
+      sP[pr * QS + (item - pr * PS)] = v[s];
+    }
+  }
+  __syncthreads();
+  // a thread owns channels ch = tid, tid + 256, ... of every row: the channel -> (level, window tap) decode is done
+  // once, then the QB rows are written with 64 lanes on 64 consecutive floats per store
+  const int nq = min(QB, a.total - q0);
+  float* dst = a.out + (long long)q0 * row_floats;
+  for (int ch = threadIdx.x; ch < row_floats; ch += kThreads) {
+    const int lvl = ch / LS, k = ch - lvl * LS;
+    const bool real = lvl < a.nlev && k < KK;
+    const int i = k / K, j = k - i * K;  // i moves x, j moves y (Q1)
+    const int poff = j * PK + i;
+    for (int qi = 0; qi < nq; ++qi) {
+      float val = 0.f;
+      if (real) {
+        const int pr = lvl * QB + qi;
+        const float* p = &sP[pr * QS + poff];
+        const float4 w = sW[pr];
+        val = p[0] * w.x + p[1] * w.y + p[PK] * w.z + p[PK + 1] * w.w;
+      }
+      dst[(long long)qi * row_floats + ch] = val;
+    }
+  }
+}
+
 template <int R>
 int launch_lookup(const LookupArgs& a, hipStream_t s, bool tiled, bool s32) {
   dim3 grid(((a.nqb + 7) / 8) * 8 * a.nlev);
@@ -268,4 +360,42 @@ extern "C" int oflow_corr_lookup_tiled_s32(const float* const* d_levels, const i
   if ((out_pixel_stride & 127) || ((uintptr_t)d_out & 15)) return OFLOW_E_ALIGN;
   return corr_lookup_impl(d_levels, level_h, level_w, num_levels, d_coords, B, H, W, radius, nullptr, stream, true,
                           static_cast<uint8_t*>(d_out), out_pixel_stride);
+}
+
+extern "C" int oflow_corr_lookup_tiled_nhwc_f32(const float* const* d_levels, const int* level_h, const int* level_w,
+                                                int num_levels, const float* d_coords, int B, int H, int W, int radius,
+                                                float* d_out, int row_floats, void* stream) {
+  if (!d_levels || !level_h || !level_w || !d_coords || !d_out) return OFLOW_E_NULL;
+  if (B <= 0 || H <= 0 || W <= 0) return OFLOW_E_SHAPE;
+  if (num_levels < 1 || num_levels > OFLOW_MAX_LEVELS) return OFLOW_E_LEVELS;
+  if (radius < 0 || radius > OFLOW_MAX_RADIUS) return OFLOW_E_RADIUS;
+  const int K = 2 * radius + 1, LS = (K * K + 7) / 8 * 8;
+  if (row_floats < num_levels * LS || (row_floats & 31) || ((uintptr_t)d_out & 15)) return OFLOW_E_SHAPE;
+  if ((long long)B * H * W * row_floats >= (1ll << 31)) return OFLOW_E_SHAPE;
+  LookupArgs a{};
+  for (int l = 0; l < num_levels; ++l) {
+    if (!d_levels[l]) return OFLOW_E_NULL;
+    if (level_h[l] < 2 || level_w[l] < 2) return OFLOW_E_TINY;  // Q3
+    a.lv[l] = d_levels[l];
+    a.Hl[l] = level_h[l];
+    a.Wl[l] = level_w[l];
+    a.HB[l] = (level_h[l] + 3) / 4;
+    a.WB[l] = (level_w[l] + 7) / 8;
+  }
+  a.coords = d_coords;
+  a.out = d_out;
+  a.N = H * W;
+  a.total = B * H * W;
+  a.nlev = num_levels;
+  const int QB = kQ / num_levels;
+  dim3 grid((a.total + QB - 1) / QB);
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  switch (radius) {
+#define OFLOW_CASE(RR) \
+  case RR: hipLaunchKernelGGL((corr_lookup_nhwc_kernel<RR>), grid, dim3(kThreads), 0, s, a, QB, row_floats); break;
+    OFLOW_CASE(0) OFLOW_CASE(1) OFLOW_CASE(2) OFLOW_CASE(3) OFLOW_CASE(4) OFLOW_CASE(5) OFLOW_CASE(6) OFLOW_CASE(7)
+#undef OFLOW_CASE
+    default: return OFLOW_E_RADIUS;
+  }
+  return launch_status();
 }

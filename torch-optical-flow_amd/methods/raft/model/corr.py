@@ -56,6 +56,21 @@ class CorrBlock:
         corr = _native.corr_lookup(self._pyramid, coords, self.radius)
         return _native.pack_lookup_s32(corr, self.num_levels, self.radius, out)
 
+    def lookup_nhwc(self, coords: Tensor, out: Tensor) -> Tensor:
+        """The lookup as fp32 NHWC rows [B*H*W, row] in the S32 layout's channel order (an addition; the RAFT forward's
+        convc1 input): exactly ``__call__``'s values, zeros in the padding channels."""
+        if self._tiled is not None:
+            return _native.corr_lookup_tiled_nhwc(self._tiled, coords, self.radius, out)
+        b, _, h, w = coords.shape
+        corr = _native.corr_lookup(self._pyramid, coords, self.radius)  # (B, L*K*K, H, W)
+        kk = (2 * self.radius + 1) ** 2
+        ls = _native.lookup_s32_stride(self.radius)
+        view = out.view(b, h, w, -1)
+        view.zero_()
+        for lvl in range(self.num_levels):
+            view[..., lvl * ls : lvl * ls + kk] = corr[:, lvl * kk : (lvl + 1) * kk].permute(0, 2, 3, 1)
+        return out
+
     @staticmethod
     def corr(fmap1: Tensor, fmap2: Tensor) -> Tensor:
         """All-pairs volume (B, H, W, 1, H, W) / sqrt(C) (`corr.py:79-87`)."""

@@ -191,7 +191,9 @@ class SplitUpdate:
         self.hx = S(b, h, w, 12, dev)
         self.rhx = S(b, h, w, 12, dev)
         levels, radius = block.corr_levels, block.corr_radius
-        self.corr = S(b, h, w, (levels * _native.lookup_s32_stride(radius) + 31) // 32, dev, zero=True)
+        self.cgroups = (levels * _native.lookup_s32_stride(radius) + 31) // 32
+        self.corr = None  # S32 lookup (AlternateCorrBlock), allocated on first use
+        self.corr_f32 = None  # fp32 NHWC lookup rows (CorrBlock), allocated on first use
         self.c1 = S(b, h, w, 8, dev)
         self.cf = S(b, h, w, 8, dev)
         self.pm = S(b, h, w, 4, dev)
@@ -235,9 +237,19 @@ class SplitUpdate:
         """One update (`update.py:150-161` + `raft.py:128-133`): coords1 is advanced IN PLACE by delta_flow.
         Returns 0.25 * mask (B, 576, H, W) fp32 when ``need_mask``, else None."""
         V, conv, w = _native.S32Slice, _native.conv_s32, self.w
-        corr_fn.lookup_s32(coords1, self.corr)
+        b, h, wd = self.shape
+        if hasattr(corr_fn, "lookup_nhwc"):  # CorrBlock: fp32 NHWC rows, split while convc1 stages them
+            if self.corr_f32 is None:
+                self.corr_f32 = torch.empty((b * h * wd, 32 * self.cgroups), device=coords1.device, dtype=torch.float32)
+            corr_fn.lookup_nhwc(coords1, self.corr_f32)
+            corr_in = _native.F32In(self.corr_f32, b, h, wd)
+        else:
+            if self.corr is None:
+                self.corr = _native.s32_empty(b, h, wd, self.cgroups, coords1.device, zero=True)
+            corr_fn.lookup_s32(coords1, self.corr)
+            corr_in = V(self.corr)
         _native.flow_prep(coords1, self.pm, (V(self.hx), 382), (V(self.rhx), 382))
-        conv(V(self.corr), w["c1"], 128, "relu", y0=V(self.c1))
+        conv(corr_in, w["c1"], 128, "relu", y0=V(self.c1))
         conv(V(self.c1), w["c2"], 64, "relu", y0=V(self.cf, 0, 6))
         conv(V(self.pm), w["f1"], 128, "relu", y0=V(self.f1))
         conv(V(self.f1), w["f2"], 64, "relu", y0=V(self.cf, 6, 2))
@@ -250,7 +262,6 @@ class SplitUpdate:
         conv(V(self.fh), w["fh2"], 32, f32=coords1, f32_accumulate=True)
         if not need_mask:
             return None
-        b, h, wd = self.shape
         mask = torch.empty((b, 576, h, wd), device=coords1.device, dtype=torch.float32)
         conv(net, w["m1"], 128, "relu", y0=V(self.fh))
         conv(V(self.fh), w["m2"], 64, out_scale=0.25, f32=mask)

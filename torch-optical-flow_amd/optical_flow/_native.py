@@ -54,6 +54,7 @@ SYMBOLS = (
     "oflow_norm_apply_s32",
     "oflow_convex_upsample_f32",
     "oflow_conv_s32_ex2",
+    "oflow_corr_lookup_tiled_nhwc_f32",
 )
 
 _lib = None
@@ -163,7 +164,9 @@ def load() -> ctypes.CDLL:
     lib.oflow_corr_lookup_otf_f16.restype = I
     lib.oflow_corr_lookup_otf_f16.argtypes = [P, PP, IP, IP, I, P, I, I, I, I, I, P, P]
     lib.oflow_conv_s32_ex2.restype = I
-    lib.oflow_conv_s32_ex2.argtypes = list(lib.oflow_conv_s32_ex.argtypes[:-1]) + [P, P, P]
+    lib.oflow_conv_s32_ex2.argtypes = list(lib.oflow_conv_s32_ex.argtypes[:-1]) + [I, P, P, P]
+    lib.oflow_corr_lookup_tiled_nhwc_f32.restype = I
+    lib.oflow_corr_lookup_tiled_nhwc_f32.argtypes = [PP, IP, IP, I, P, I, I, I, I, P, I, P]
     lib.oflow_convex_upsample_f32.restype = I
     lib.oflow_convex_upsample_f32.argtypes = [P, P, I, I, I, P, P]
     v = lib.oflow_abi_version()
@@ -607,12 +610,42 @@ class S32Slice:
         return self.t.device
 
 
+class F32In:
+    """Convolution input given as a dense fp32 NHWC tensor [B*H*W, C] (C % 32 == 0), split into hi + lo while the
+    kernel stages it (oflow_conv_s32_ex2, OFLOW_IN_F32; 1x1 convs): e.g. corr_lookup_tiled_nhwc's output."""
+
+    __slots__ = ("raw", "bhw")
+    in_format = 2
+
+    def __init__(self, raw: torch.Tensor, b: int, h: int, w: int):
+        if raw.dtype != torch.float32 or not raw.is_contiguous() or raw.shape[0] != b * h * w or raw.shape[1] % 32:
+            raise RuntimeError("F32In: raw must be contiguous fp32 [B*H*W, C], C % 32 == 0")
+        self.raw, self.bhw = raw, (int(b), int(h), int(w))
+
+    @property
+    def ptr(self) -> int:
+        return self.raw.data_ptr()
+
+    @property
+    def ps(self) -> int:
+        return int(self.raw.shape[1]) * 4
+
+    @property
+    def ng(self) -> int:
+        return int(self.raw.shape[1]) // 32
+
+    @property
+    def device(self):
+        return self.raw.device
+
+
 class NhwcNormIn:
     """Convolution input given as the previous convolution's raw fp32 NHWC output [B*H*W, C] plus its instance-norm
     affine (scale, shift: [B, C]); the kernel stages relu(raw * scale + shift) (oflow_conv_s32_ex2), so the normalised
     activation is never written to HBM."""
 
     __slots__ = ("raw", "bhw", "scale", "shift")
+    in_format = 1
 
     def __init__(self, raw: torch.Tensor, b: int, h: int, w: int, scale: torch.Tensor, shift: torch.Tensor):
         c = raw.shape[1]
@@ -718,6 +751,7 @@ def conv_s32(x: S32Slice, cw: ConvWeights, block_n: int, act: str = "none", out_
         raise RuntimeError(f"{what}: input has {x.ng} groups, weights expect {cw.kg}")
     b, h, w = x.bhw
     nin = isinstance(x, NhwcNormIn)
+    in_format = getattr(x, "in_format", 0)
     hw_out = (h // 2, w // 2) if s2d else (h, w)
     for d in (y0, y1):
         if d is not None and (tuple(d.t.shape[:3]) != (b, *hw_out) or d.t.device != x.device):
@@ -755,7 +789,7 @@ def conv_s32(x: S32Slice, cw: ConvWeights, block_n: int, act: str = "none", out_
                 nhwc.data_ptr() if nhwc is not None else None, cw.n,
                 stats.data_ptr() if stats is not None else None,
                 res.ptr if res is not None else None, res.ps if res is not None else 0, ACT[res_act], int(bool(s2d)),
-                x.scale.data_ptr() if nin else None, x.shift.data_ptr() if nin else None,
+                in_format, x.scale.data_ptr() if nin else None, x.shift.data_ptr() if nin else None,
                 _stream(dev),
             ),
             what,
@@ -870,6 +904,30 @@ def flow_prep(coords: torch.Tensor, patches: torch.Tensor, flow0=None, flow1=Non
     f1 = (flow1[0].channel_ptr(flow1[1]), flow1[0].ps) if flow1 is not None else (None, 0)
     with torch.cuda.device(co.device), _Timed("flow_prep", co.device):
         _check(load().oflow_flow_prep_s32(co.data_ptr(), b, h, w, patches.data_ptr(), f0[0], f0[1], f1[0], f1[1], _stream(co.device)), "flow_prep")
+
+
+def corr_lookup_tiled_nhwc(pyr: TiledPyramid, coords: torch.Tensor, radius: int, out: torch.Tensor) -> torch.Tensor:
+    """``corr_lookup_tiled`` as fp32 NHWC rows into ``out`` [B*H*W, row] (row % 32 == 0): level l at channels
+    [l*LS, l*LS + (2r+1)^2) (LS = lookup_s32_stride(r)), every other channel written as 0 -- convc1's input
+    (F32In), the same permuted order as the S32 layout."""
+    what = "corr_lookup"
+    co = _gpu_f32(coords, "coords", what)
+    b, _, h, w = co.shape
+    nl = len(pyr.levels)
+    if b * h * w != pyr.queries:
+        raise RuntimeError(f"{what}: coords {tuple(coords.shape)} do not match the pyramid's {pyr.queries} queries")
+    if out.dtype != torch.float32 or not out.is_contiguous() or out.dim() != 2 or out.shape[0] != b * h * w:
+        raise RuntimeError(f"{what}: NHWC output must be contiguous fp32 [B*H*W, row]")
+    ptrs = (ctypes.c_void_p * nl)(*[t.data_ptr() for t in pyr.levels])
+    hs = (ctypes.c_int * nl)(*[d[0] for d in pyr.dims])
+    ws = (ctypes.c_int * nl)(*[d[1] for d in pyr.dims])
+    with torch.cuda.device(co.device), _Timed("corr_lookup", co.device):
+        _check(
+            load().oflow_corr_lookup_tiled_nhwc_f32(ptrs, hs, ws, nl, co.data_ptr(), b, h, w, int(radius), out.data_ptr(),
+                                                    int(out.shape[1]), _stream(co.device)),
+            what,
+        )
+    return out
 
 
 def corr_lookup_tiled_s32(pyr: TiledPyramid, coords: torch.Tensor, radius: int, out: torch.Tensor) -> torch.Tensor:
