@@ -250,6 +250,20 @@ int oflow_norm_apply_s32(const float* d_x, int C, int B, int H, int W, const flo
  */
 int oflow_convex_upsample_f32(const float* d_flow, const float* d_mask, int B, int H, int W, float* d_out, void* stream);
 
+/*
+ * Backward of the correlation (methods/raft/model/corr.py:38-87 + utils.py:64-80 under autograd, the training step
+ * raft.py:149-175; csrc/corr_backward.hip). Canonical levels (B*H*W, H_l, W_l) fp32.
+ * oflow_corr_lookup_backward_f32: d_grad_out (B, L*(2r+1)^2, H, W) -> d_grad_levels[l] += its gradient (same window
+ *   and weights as the forward; coordinates get none: the reference detaches them, raft.py:127).
+ * oflow_corr_pyramid_grad_combine_f32: d_grad_levels[0] += sum_{l>0} of level l's gradient pushed back through the
+ *   floor 2x2 average pools (value / 4^l on every level-0 cell it averaged).
+ */
+int oflow_corr_lookup_backward_f32(const float* d_grad_out, const float* d_coords, int B, int H, int W, int radius,
+                                   float* const* d_grad_levels, const int* level_h, const int* level_w, int num_levels,
+                                   void* stream);
+int oflow_corr_pyramid_grad_combine_f32(float* const* d_grad_levels, const int* level_h, const int* level_w,
+                                        int num_levels, long long Q, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -207,6 +207,7 @@ class RAFT(nn.Module):
         preds = []
         flow_up = None
         for _ in range(iters):
+            coords1 = coords1.detach()  # raft.py:127 (no effect on the values; gradients stop here as in the reference)
             corr = corr_lookup(pyramid, coords1, self.corr_radius)
             net, up_mask, delta = self.update_block(net, inp, corr, coords1 - coords0)
             coords1 = coords1 + delta

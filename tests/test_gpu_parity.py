@@ -318,14 +318,30 @@ def test_corrblock_pyramid_attribute_semantics():
 
 
 def test_ops_refuse_autograd_inputs():
-    """No backward kernels (SURVEY §8(f) row 3): an input that requires grad must raise, not silently drop the graph;
-    under no_grad the same call runs."""
+    """The raw native ops have no autograd: an input that requires grad must raise, not silently drop the graph
+    (CorrBlock and optical_flow.warp wrap them in autograd Functions instead); under no_grad the same call runs."""
     f = torch.randn(1, 8, 16, 16, device=DEV, requires_grad=True)
     with pytest.raises(RuntimeError, match="requires grad"):
-        CorrBlock(f, f.detach())
+        _native.corr_pyramid(f, f.detach(), 1)
     frame = torch.rand(1, 3, 8, 8, device=DEV, requires_grad=True)
     flow = torch.zeros(1, 2, 8, 8, device=DEV)
     with pytest.raises(RuntimeError, match="requires grad"):
-        optical_flow.warp(frame, flow)
+        _native.grid_warp(frame, flow, "bilinear", "border", False)
     with torch.no_grad():
         assert optical_flow.warp(frame, flow).shape == frame.shape
+
+
+@pytest.mark.parametrize("pad", ["zeros", "border", "reflection"])
+def test_warp_autograd_matches_oracle(pad):
+    """optical_flow.warp under autograd: HIP forward, grid_sampler backward -- frame and flow gradients equal the
+    reference operator's (operator.py:8-56) on the CPU."""
+    img0, _ = synthetic.synthetic_pair(2, 40, 64, seed=9)
+    flow = oop.normalize(torch.from_numpy(synthetic.hash_normal(13, (2, 2, 40, 64), 3.0)))
+    r = torch.from_numpy(synthetic.hash_normal(14, (2, 3, 40, 64), 1.0))
+    a_f, a_w = img0.clone().requires_grad_(), flow.clone().requires_grad_()
+    (oop.warp(a_f, a_w, "bilinear", pad, False) * r).sum().backward()
+    d_f, d_w = img0.to(DEV).requires_grad_(), flow.to(DEV).requires_grad_()
+    (optical_flow.warp(d_f, d_w, "bilinear", pad) * r.to(DEV)).sum().backward()
+    assert float((d_f.grad.cpu() - a_f.grad).abs().max()) <= 1e-4
+    gw = float(a_w.grad.abs().max())
+    assert float((d_w.grad.cpu() - a_w.grad).abs().max()) <= 1e-3 * gw + 1e-3

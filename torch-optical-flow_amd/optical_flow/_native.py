@@ -55,6 +55,8 @@ SYMBOLS = (
     "oflow_convex_upsample_f32",
     "oflow_conv_s32_ex2",
     "oflow_corr_lookup_tiled_nhwc_f32",
+    "oflow_corr_lookup_backward_f32",
+    "oflow_corr_pyramid_grad_combine_f32",
 )
 
 _lib = None
@@ -165,6 +167,10 @@ def load() -> ctypes.CDLL:
     lib.oflow_corr_lookup_otf_f16.argtypes = [P, PP, IP, IP, I, P, I, I, I, I, I, P, P]
     lib.oflow_conv_s32_ex2.restype = I
     lib.oflow_conv_s32_ex2.argtypes = list(lib.oflow_conv_s32_ex.argtypes[:-1]) + [I, P, P, P]
+    lib.oflow_corr_lookup_backward_f32.restype = I
+    lib.oflow_corr_lookup_backward_f32.argtypes = [P, P, I, I, I, I, PP, IP, IP, I, P]
+    lib.oflow_corr_pyramid_grad_combine_f32.restype = I
+    lib.oflow_corr_pyramid_grad_combine_f32.argtypes = [PP, IP, IP, I, L, P]
     lib.oflow_corr_lookup_tiled_nhwc_f32.restype = I
     lib.oflow_corr_lookup_tiled_nhwc_f32.argtypes = [PP, IP, IP, I, P, I, I, I, I, P, I, P]
     lib.oflow_convex_upsample_f32.restype = I
@@ -904,6 +910,44 @@ def flow_prep(coords: torch.Tensor, patches: torch.Tensor, flow0=None, flow1=Non
     f1 = (flow1[0].channel_ptr(flow1[1]), flow1[0].ps) if flow1 is not None else (None, 0)
     with torch.cuda.device(co.device), _Timed("flow_prep", co.device):
         _check(load().oflow_flow_prep_s32(co.data_ptr(), b, h, w, patches.data_ptr(), f0[0], f0[1], f1[0], f1[1], _stream(co.device)), "flow_prep")
+
+
+def corr_lookup_backward(grad_out: torch.Tensor, coords: torch.Tensor, radius: int, grads) -> None:
+    """Accumulate the lookup's input gradient into ``grads`` (canonical levels (B*H*W, 1, H_l, W_l) fp32, contiguous):
+    the transpose of corr_lookup for the same coords (which get no gradient, as in the reference)."""
+    what = "corr_lookup_backward"
+    go = _gpu_f32(grad_out, "grad_out", what)
+    co = _gpu_f32(coords, "coords", what)
+    b, _, h, w = co.shape
+    nl = len(grads)
+    for g in grads:
+        if g.dtype != torch.float32 or not g.is_contiguous() or g.shape[0] != b * h * w or g.device != co.device:
+            raise RuntimeError(f"{what}: gradient levels must be contiguous fp32 (B*H*W, 1, H_l, W_l)")
+    k = 2 * int(radius) + 1
+    if tuple(go.shape) != (b, nl * k * k, h, w):
+        raise RuntimeError(f"{what}: grad_out {tuple(go.shape)} does not match coords / levels")
+    ptrs = (ctypes.c_void_p * nl)(*[g.data_ptr() for g in grads])
+    hs = (ctypes.c_int * nl)(*[int(g.shape[-2]) for g in grads])
+    ws = (ctypes.c_int * nl)(*[int(g.shape[-1]) for g in grads])
+    with torch.cuda.device(co.device):
+        _check(load().oflow_corr_lookup_backward_f32(go.data_ptr(), co.data_ptr(), b, h, w, int(radius), ptrs, hs, ws, nl,
+                                                     _stream(co.device)), what)
+
+
+def pyramid_grad_combine(grads) -> torch.Tensor:
+    """grads[0] += every coarser level's gradient pushed back through the floor 2x2 average pools; returns grads[0]."""
+    what = "corr_pyramid_backward"
+    nl = len(grads)
+    q = int(grads[0].shape[0])
+    for g in grads:
+        if g.dtype != torch.float32 or not g.is_contiguous() or g.shape[0] != q or g.device.type != "cuda":
+            raise RuntimeError(f"{what}: gradient levels must be contiguous fp32 CUDA (Q, 1, H_l, W_l)")
+    ptrs = (ctypes.c_void_p * nl)(*[g.data_ptr() for g in grads])
+    hs = (ctypes.c_int * nl)(*[int(g.shape[-2]) for g in grads])
+    ws = (ctypes.c_int * nl)(*[int(g.shape[-1]) for g in grads])
+    with torch.cuda.device(grads[0].device):
+        _check(load().oflow_corr_pyramid_grad_combine_f32(ptrs, hs, ws, nl, q, _stream(grads[0].device)), what)
+    return grads[0]
 
 
 def corr_lookup_tiled_nhwc(pyr: TiledPyramid, coords: torch.Tensor, radius: int, out: torch.Tensor) -> torch.Tensor:
