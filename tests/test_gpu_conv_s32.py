@@ -264,3 +264,20 @@ def test_conv_f32_input_equals_s32_input():
     N.conv_s32(N.F32In(x, b, h, w), cw, 128, "relu", y0=N.S32Slice(y2))
     torch.cuda.synchronize()
     assert torch.equal(y1, y2)
+
+
+@pytest.mark.parametrize("b,c,h,w", [(2, 3, 40, 70), (1, 3, 9, 131), (1, 1, 16, 16)])
+def test_stem_patches_match_unfold(b, c, h, w):
+    """oflow_stem_patches_s32 (LDS-staged 7x7/2 pad-3 patch matrix, channel t*C + c) = F.unfold of the image, as
+    hi + lo (exact for these small integers), zeros past 49*C; ragged last workgroup (Wo % 64 != 0)."""
+    g = torch.Generator().manual_seed(b * 100 + w)
+    img = torch.randint(0, 256, (b, c, h, w), generator=g).float().to(DEV)
+    groups = (49 * c + 31) // 32
+    out = N.s32_empty(b, (h + 1) // 2, (w + 1) // 2, groups, DEV)
+    N.stem_patches(img, out)
+    got = N.s32_to_f32(out)  # (B, G*32, Ho, Wo)
+    ho, wo = (h + 1) // 2, (w + 1) // 2
+    unf = F.unfold(img, 7, padding=3, stride=2).view(b, c, 49, ho, wo)  # channel c*49 + t
+    ref = unf.permute(0, 2, 1, 3, 4).reshape(b, 49 * c, ho, wo)  # -> t*C + c
+    assert torch.equal(got[:, : 49 * c], ref)
+    assert bool((got[:, 49 * c :] == 0).all())

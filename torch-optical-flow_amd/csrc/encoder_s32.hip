@@ -37,35 +37,62 @@ __device__ __forceinline__ void put8(uint8_t* line, const float* v) {
   *reinterpret_cast<half8*>(line + 64) = lo;
 }
 
-// one thread = one output pixel x one 32-channel group of the patch matrix
-__global__ __launch_bounds__(256) void stem_patches_kernel(const float* __restrict__ img, int B, int C, int H, int W,
-                                                           int Ho, int Wo, int G, uint8_t* out) {
-  constexpr int KS = 7, PAD = 3, ST = 2;
-  const long long P = (long long)B * Ho * Wo;
-  const long long item = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (item >= P * G) return;
-  const int g = static_cast<int>(item % G);
-  const long long p = item / G;
-  const int b = static_cast<int>(p / ((long long)Ho * Wo));
-  const int pix = static_cast<int>(p - (long long)b * Ho * Wo);
-  const int oy = pix / Wo, ox = pix - oy * Wo;
+// One workgroup = 64 consecutive output pixels of one output row: the 7 input rows x (2*64 + 5) input columns x C
+// channels they read are staged in LDS once (coalesced row reads, zero padding applied there), then each thread
+// assembles (pixel, 32-channel group) lines from LDS; the workgroup's output is one contiguous run of 64 * G lines.
+constexpr int kStemPX = 64, kStemMaxC = 4;
+template <int C>  // input channels: compile-time, so the channel / tap decode of every patch entry is constant folded
+__global__ __launch_bounds__(256) void stem_patches_kernel(const float* __restrict__ img, int B, int H, int W, int Ho,
+                                                           int Wo, int G, uint8_t* out) {
+  constexpr int KS = 7, PAD = 3, ST = 2, IX = ST * kStemPX + KS - ST;  // 133 input columns
+  __shared__ float sImg[C][KS][IX];
+  const int xb = blockIdx.x, oy = blockIdx.y, b = blockIdx.z;
+  const int ox0 = xb * kStemPX;
+  const int iy0 = oy * ST - PAD, ix0 = ox0 * ST - PAD;
   const float* src = img + (long long)b * C * H * W;
-  float v[32];
-#pragma unroll
-  for (int e = 0; e < 32; ++e) {
-    const int k = g * 32 + e;
-    const int t = k / C, c = k - t * C;
-    float val = 0.f;
-    if (t < KS * KS) {
-      const int iy = oy * ST - PAD + t / KS, ix = ox * ST - PAD + t % KS;
-      if (static_cast<unsigned>(iy) < static_cast<unsigned>(H) && static_cast<unsigned>(ix) < static_cast<unsigned>(W))
-        val = src[((long long)c * H + iy) * W + ix];
-    }
-    v[e] = val;
+  for (int e = threadIdx.x; e < C * KS * IX; e += 256) {
+    const int c = e / (KS * IX), rem = e - c * (KS * IX);
+    const int ky = rem / IX, xx = rem - ky * IX;
+    const int iy = iy0 + ky, ix = ix0 + xx;
+    float v = 0.f;
+    if (static_cast<unsigned>(iy) < static_cast<unsigned>(H) && static_cast<unsigned>(ix) < static_cast<unsigned>(W))
+      v = src[((long long)c * H + iy) * W + ix];
+    sImg[c][ky][xx] = v;
   }
-  uint8_t* line = out + (p * G + g) * 128;
+  __syncthreads();
+  const int npx = min(kStemPX, Wo - ox0);
+  uint8_t* dst = out + (((long long)b * Ho + oy) * Wo + ox0) * G * 128;
+  // lane = one 16-B piece of a line (8 hi or 8 lo halves): 8 consecutive lanes fill one 128-B line, so every store
+  // instruction writes 8 whole consecutive lines
+  for (int item = threadIdx.x; item < npx * G * 8; item += 256) {
+    const int line = item >> 3, piece = item & 7, q = piece & 3;
+    const int px = line / G, g = line - px * G;
+    float v[8];
 #pragma unroll
-  for (int q = 0; q < 4; ++q) put8(line + q * 16, v + 8 * q);
+    for (int e = 0; e < 8; ++e) v[e] = 0.f;
+    // the (group, quarter) of a lane is divergent within a wave, the 8 entries it needs are not: one body per pair
+#pragma unroll
+    for (int gg = 0; gg < (KS * KS * C + 31) / 32; ++gg) {
+#pragma unroll
+      for (int qq = 0; qq < 4; ++qq) {
+        if (g == gg && q == qq) {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            const int k = gg * 32 + qq * 8 + e;
+            const int t = k / C, c = k - t * C;
+            if (t < KS * KS) v[e] = sImg[c][t / KS][px * ST + t % KS];
+          }
+        }
+      }
+    }
+    half8 h;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const _Float16 a = static_cast<_Float16>(v[e]);
+      h[e] = piece < 4 ? a : static_cast<_Float16>(v[e] - static_cast<float>(a));
+    }
+    *reinterpret_cast<half8*>(dst + (long long)line * 128 + (piece < 4 ? q * 16 : 64 + q * 16)) = h;
+  }
 }
 
 // one workgroup = one image x 64 channels, 1024 threads: lane = channel (coalesced 12-B partials), the 16 waves stride
@@ -187,10 +214,18 @@ extern "C" int oflow_stem_patches_s32(const float* d_img, int B, int C, int H, i
   if (!d_img || !d_out) return OFLOW_E_NULL;
   if (B <= 0 || C <= 0 || H <= 0 || W <= 0 || out_groups * 32 < 49 * C) return OFLOW_E_SHAPE;
   if ((uintptr_t)d_out & 15) return OFLOW_E_ALIGN;
+  if (C > kStemMaxC || B > 65535) return OFLOW_E_SHAPE;
   const int Ho = (H - 1) / 2 + 1, Wo = (W - 1) / 2 + 1;  // (H + 2*3 - 7) / 2 + 1
-  const long long items = (long long)B * Ho * Wo * out_groups;
-  hipLaunchKernelGGL(stem_patches_kernel, dim3((unsigned)((items + 255) / 256)), dim3(256), 0,
-                     static_cast<hipStream_t>(stream), d_img, B, C, H, W, Ho, Wo, out_groups, static_cast<uint8_t*>(d_out));
+  if (Ho > 65535) return OFLOW_E_SHAPE;
+  const dim3 grid((Wo + kStemPX - 1) / kStemPX, Ho, B);
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  uint8_t* o = static_cast<uint8_t*>(d_out);
+  switch (C) {
+    case 1: hipLaunchKernelGGL(stem_patches_kernel<1>, grid, dim3(256), 0, s, d_img, B, H, W, Ho, Wo, out_groups, o); break;
+    case 2: hipLaunchKernelGGL(stem_patches_kernel<2>, grid, dim3(256), 0, s, d_img, B, H, W, Ho, Wo, out_groups, o); break;
+    case 3: hipLaunchKernelGGL(stem_patches_kernel<3>, grid, dim3(256), 0, s, d_img, B, H, W, Ho, Wo, out_groups, o); break;
+    default: hipLaunchKernelGGL(stem_patches_kernel<4>, grid, dim3(256), 0, s, d_img, B, H, W, Ho, Wo, out_groups, o); break;
+  }
   return launch_status();
 }
 
