@@ -9,7 +9,7 @@ stride-2 stages fed in space-to-depth layout. ``SmallEncoder``/``BottleneckBlock
 """
 from __future__ import annotations
 
-from typing import List, Sequence, Tuple, Union
+from typing import Optional, List, Sequence, Tuple, Union
 
 import torch
 import torch.nn as nn
@@ -222,7 +222,9 @@ class SplitEncoder:
             return _native.NhwcNormIn(raw, *shape, alpha, beta)
         return _native.S32Slice(self._conv_norm(x, cw, shape, "relu"))
 
-    def __call__(self, x: Union[Tensor, Sequence[Tensor]]) -> Union[Tensor, Tuple[Tensor, ...]]:
+    def __call__(self, x: Union[Tensor, Sequence[Tensor]], patches: Optional[Tensor] = None) -> Union[Tensor, Tuple[Tensor, ...]]:
+        """``patches``: the stem's patch matrix of ``x`` when another encoder already built it (RAFT's cnet reads
+        image0's rows of fnet's, raft.py:109/115); the one built here is kept as ``self.patches``."""
         is_list = isinstance(x, (tuple, list))
         if is_list:
             batch_dim = x[0].shape[0]
@@ -234,8 +236,10 @@ class SplitEncoder:
         V = _native.S32Slice
         dev = x.device
         h, w = hh // 2, ww // 2
-        patches = _native.s32_empty(n, h, w, self.w["stem"].kg, dev)
-        _native.stem_patches(x, patches)
+        if patches is None or tuple(patches.shape[:4]) != (n, h, w, self.w["stem"].kg):
+            patches = _native.s32_empty(n, h, w, self.w["stem"].kg, dev)
+            _native.stem_patches(x, patches)
+        self.patches = patches
         cur = self._conv_norm(V(patches), self.w["stem"], (n, h, w), "relu")
         layers = (self.enc.layer1, self.enc.layer2, self.enc.layer3)
         for li, layer in enumerate(layers):

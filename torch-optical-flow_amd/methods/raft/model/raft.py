@@ -158,7 +158,10 @@ class RAFT(nn.Module):
         block = AlternateCorrBlock if self.hparams.get("alternate_corr", False) else CorrBlock
         corr_fn = block(fmap1.float(), fmap2.float(), radius=self.hparams.corr_radius)
 
-        cnet_out = cnet(image0)
+        if split_enc and isinstance(cnet, SplitEncoder):  # image0's stem patches are fnet's first rows
+            cnet_out = cnet(image0, patches=fnet.patches[: image0.shape[0]])
+        else:
+            cnet_out = cnet(image0)
         coords0, coords1 = self.initialize_flow(image0)
         if flow_init is not None:
             coords1 = coords1 + flow_init
