@@ -1,0 +1,49 @@
+"""EXPERIMENT: RAFT Sintel x8 forward with / without the motion encoder's side stream, interleaved in one process."""
+import os
+import statistics
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(os.path.dirname(HERE))
+PKG = os.path.join(REPO, "torch-optical-flow_amd")
+for p in (REPO, PKG, os.path.join(PKG, "methods", "raft")):
+    sys.path.insert(0, p)
+
+import torch  # noqa: E402
+
+from model import RAFT, InputPadder, synthetic  # noqa: E402
+
+
+def main():
+    dev = torch.device("cuda", 0)
+    torch.backends.cudnn.benchmark = True
+    model = RAFT().eval()
+    model.load_state_dict(synthetic.synthetic_state_dict(model.state_dict()))
+    model = model.to(dev)
+    a0, a1 = synthetic.synthetic_pair(2, 436, 1024, seed=0)
+    img0 = a0.to(dev).repeat(4, 1, 1, 1)
+    img1 = a1.to(dev).repeat(4, 1, 1, 1)
+    padder = InputPadder((436, 1024), mode="sintel")
+    p0, p1 = padder.pad(img0, img1)
+    res = {True: [], False: []}
+    with torch.inference_mode():
+        for flag in (True, False):
+            model.update_block.split_streams = flag
+            model(p0, p1, iters=12, test_mode=True)
+        torch.cuda.synchronize()
+        for _ in range(6):
+            for flag in (True, False):
+                model.update_block.split_streams = flag
+                a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                a.record()
+                for _ in range(3):
+                    model(p0, p1, iters=12, test_mode=True)
+                b.record()
+                b.synchronize()
+                res[flag].append(a.elapsed_time(b) / 3)
+    for flag, v in res.items():
+        print(f"streams={flag}: median {statistics.median(v):.3f} ms/step, min {min(v):.3f}", flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -158,6 +158,16 @@ class FusedUpdate:
         return net, mask, delta_flow
 
 
+_SIDE_STREAMS = {}
+
+
+def _side_stream(device: torch.device) -> "torch.cuda.Stream":
+    key = torch.device(device).index
+    if key not in _SIDE_STREAMS:
+        _SIDE_STREAMS[key] = torch.cuda.Stream(device=device)
+    return _SIDE_STREAMS[key]
+
+
 def _weights_key(block: nn.Module):
     return tuple((q.data_ptr(), q._version) for q in block.parameters())
 
@@ -205,6 +215,9 @@ class SplitUpdate:
         _native.pack_s32(cnet_out[:, :hdim], "tanh", V(self.hx, 0, 4), nhwc=self.hm)  # raft.py:117
         _native.pack_s32(cnet_out[:, hdim:], "relu", V(self.hx, 4, 4), V(self.rhx, 4, 4))  # raft.py:118
         self.w = self._weights(block)
+        # side stream for the motion encoder's flow branch (one per device, reused across forwards)
+        self.streams = getattr(block, "split_streams", True)
+        self.side_stream = _side_stream(dev) if self.streams else None
 
     @staticmethod
     def _weights(block: BasicUpdateBlock):
@@ -248,11 +261,28 @@ class SplitUpdate:
                 self.corr = _native.s32_empty(b, h, wd, self.cgroups, coords1.device, zero=True)
             corr_fn.lookup_s32(coords1, self.corr)
             corr_in = V(self.corr)
-        _native.flow_prep(coords1, self.pm, (V(self.hx), 382), (V(self.rhx), 382))
-        conv(corr_in, w["c1"], 128, "relu", y0=V(self.c1))
-        conv(V(self.c1), w["c2"], 64, "relu", y0=V(self.cf, 0, 6))
-        conv(V(self.pm), w["f1"], 128, "relu", y0=V(self.f1))
-        conv(V(self.f1), w["f2"], 64, "relu", y0=V(self.cf, 6, 2))
+        # The motion encoder's two branches are independent (update.py:116-121): the flow branch (flow prep, convf1,
+        # convf2) runs on a side stream beside the correlation branch (convc1, convc2), both MFMA-latency bound, and
+        # joins before the motion conv. The side stream starts after the lookup, which thus runs alone (its bench
+        # timing stays uncontended). Buffers are persistent and disjoint (cf groups 6-7 vs 0-5; the GRU inputs' flow
+        # group is read again only after the join).
+        main = torch.cuda.current_stream(coords1.device)
+        side = self.side_stream if self.streams else None
+        if side is not None:
+            side.wait_stream(main)
+            with torch.cuda.stream(side):
+                _native.flow_prep(coords1, self.pm, (V(self.hx), 382), (V(self.rhx), 382))
+                conv(V(self.pm), w["f1"], 128, "relu", y0=V(self.f1))
+                conv(V(self.f1), w["f2"], 64, "relu", y0=V(self.cf, 6, 2))
+            conv(corr_in, w["c1"], 128, "relu", y0=V(self.c1))
+            conv(V(self.c1), w["c2"], 64, "relu", y0=V(self.cf, 0, 6))
+            main.wait_stream(side)
+        else:
+            _native.flow_prep(coords1, self.pm, (V(self.hx), 382), (V(self.rhx), 382))
+            conv(corr_in, w["c1"], 128, "relu", y0=V(self.c1))
+            conv(V(self.c1), w["c2"], 64, "relu", y0=V(self.cf, 0, 6))
+            conv(V(self.pm), w["f1"], 128, "relu", y0=V(self.f1))
+            conv(V(self.f1), w["f2"], 64, "relu", y0=V(self.cf, 6, 2))
         conv(V(self.cf), w["mo"], 128, "relu", y0=V(self.hx, 8, 4), y1=V(self.rhx, 8, 4))
         for tag in ("1", "2"):
             conv(V(self.hx), w["zr" + tag], 128, epilogue=1, y0=V(self.rhx, 0, 4), gru_h=self.hm, gru_z=self.z)
