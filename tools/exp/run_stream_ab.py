@@ -25,24 +25,35 @@ def main():
     img1 = a1.to(dev).repeat(4, 1, 1, 1)
     padder = InputPadder((436, 1024), mode="sintel")
     p0, p1 = padder.pad(img0, img1)
-    res = {True: [], False: []}
+    cfgs = {"enc+update": (True, True), "update only": (False, True), "none": (False, False)}
+    res = {k: [] for k in cfgs}
+
+    def setf(k):
+        model.encoder_streams, model.update_block.split_streams = cfgs[k]
+
     with torch.inference_mode():
-        for flag in (True, False):
-            model.update_block.split_streams = flag
+        for k in cfgs:
+            setf(k)
             model(p0, p1, iters=12, test_mode=True)
         torch.cuda.synchronize()
+        outs = {}
+        for k in cfgs:
+            setf(k)
+            outs[k] = model(p0, p1, iters=12, test_mode=True)[1].clone()
+        torch.cuda.synchronize()
+        print("outputs equal across stream configs:", all(torch.equal(outs[k], outs["none"]) for k in cfgs), flush=True)
         for _ in range(6):
-            for flag in (True, False):
-                model.update_block.split_streams = flag
+            for k in cfgs:
+                setf(k)
                 a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 a.record()
                 for _ in range(3):
                     model(p0, p1, iters=12, test_mode=True)
                 b.record()
                 b.synchronize()
-                res[flag].append(a.elapsed_time(b) / 3)
-    for flag, v in res.items():
-        print(f"streams={flag}: median {statistics.median(v):.3f} ms/step, min {min(v):.3f}", flush=True)
+                res[k].append(a.elapsed_time(b) / 3)
+    for k, v in res.items():
+        print(f"streams={k}: median {statistics.median(v):.3f} ms/step, min {min(v):.3f}", flush=True)
 
 
 if __name__ == "__main__":

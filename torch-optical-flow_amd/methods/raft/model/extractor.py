@@ -222,6 +222,14 @@ class SplitEncoder:
             return _native.NhwcNormIn(raw, *shape, alpha, beta)
         return _native.S32Slice(self._conv_norm(x, cw, shape, "relu"))
 
+    def stem_patches(self, x: Tensor) -> Tensor:
+        """The stem's 7x7/2 patch matrix (S32) of a (n, 3, H, W) input, as ``__call__`` would build it."""
+        x = x.float().contiguous()
+        n, _, hh, ww = x.shape
+        patches = _native.s32_empty(n, hh // 2, ww // 2, self.w["stem"].kg, x.device)
+        _native.stem_patches(x, patches)
+        return patches
+
     def __call__(self, x: Union[Tensor, Sequence[Tensor]], patches: Optional[Tensor] = None) -> Union[Tensor, Tuple[Tensor, ...]]:
         """``patches``: the stem's patch matrix of ``x`` when another encoder already built it (RAFT's cnet reads
         image0's rows of fnet's, raft.py:109/115); the one built here is kept as ``self.patches``."""

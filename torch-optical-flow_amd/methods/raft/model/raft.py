@@ -32,7 +32,7 @@ from optical_flow import _native
 
 from .corr import AlternateCorrBlock, CorrBlock
 from .extractor import BasicEncoder, SplitEncoder
-from .update import BasicUpdateBlock, FusedUpdate, SplitUpdate
+from .update import BasicUpdateBlock, FusedUpdate, SplitUpdate, _side_stream
 from .utils import coords_grid, upflow8
 
 
@@ -92,6 +92,7 @@ class RAFT(nn.Module):
         self.fused_update = True
         # "split": encoders on the split-fp16 kernels (SplitEncoder) in GPU inference; "module": nn.Module (MIOpen)
         self.encoder_impl = "split"
+        self.encoder_streams = True  # cnet beside fnet + the corr pyramid (inference, split encoders)
 
     # -- checkpoints -------------------------------------------------------------------------------------
     @classmethod
@@ -154,13 +155,26 @@ class RAFT(nn.Module):
         split_enc = image0.is_cuda and not torch.is_grad_enabled() and self.encoder_impl == "split"
         fnet = SplitEncoder(self.fnet) if split_enc else self.fnet
         cnet = SplitEncoder(self.cnet) if split_enc and not self.cnet.training else self.cnet
-        fmap1, fmap2 = fnet([image0, image1])
         block = AlternateCorrBlock if self.hparams.get("alternate_corr", False) else CorrBlock
-        corr_fn = block(fmap1.float(), fmap2.float(), radius=self.hparams.corr_radius)
-
-        if split_enc and isinstance(cnet, SplitEncoder):  # image0's stem patches are fnet's first rows
-            cnet_out = cnet(image0, patches=fnet.patches[: image0.shape[0]])
+        if split_enc and isinstance(cnet, SplitEncoder):
+            # image0's stem patches are the first rows of fnet's (raft.py:109, 115 feed both the same image0); cnet
+            # runs on a side stream beside fnet and the correlation pyramid, joined before the update loop
+            patches = fnet.stem_patches(torch.cat([image0, image1], dim=0))
+            main = torch.cuda.current_stream(image0.device)
+            side = _side_stream(image0.device) if self.encoder_streams else None
+            if side is not None:
+                side.wait_stream(main)
+                with torch.cuda.stream(side):
+                    cnet_out = cnet(image0, patches=patches[: image0.shape[0]])
+            fmap1, fmap2 = fnet([image0, image1], patches=patches)
+            corr_fn = block(fmap1.float(), fmap2.float(), radius=self.hparams.corr_radius)
+            if side is not None:
+                main.wait_stream(side)
+            else:
+                cnet_out = cnet(image0, patches=patches[: image0.shape[0]])
         else:
+            fmap1, fmap2 = fnet([image0, image1])
+            corr_fn = block(fmap1.float(), fmap2.float(), radius=self.hparams.corr_radius)
             cnet_out = cnet(image0)
         coords0, coords1 = self.initialize_flow(image0)
         if flow_init is not None:
