@@ -268,6 +268,7 @@ def main() -> int:
             line["kernels"] = {
                 "corr_pyramid": {
                     "bound": "mfma",
+                    "note": "in-step: runs beside cnet (side stream); alone: tools/kbench.py",
                     "launch_ms": round(pk_ms, 4),
                     "achieved_tflops": round(tf, 2),
                     "peak_tflops": MFMA_F32_PEAK_TFLOPS,
