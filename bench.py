@@ -241,7 +241,8 @@ def main() -> int:
         lk = rec.get("corr_lookup", [])
         pk = rec.get("corr_pyramid", [])
         lk_ms = mean_ms(lk)
-        lk_bytes = lookup_bytes(ppg, dims)
+        # per launch: a step does `iters` full-batch lookups' worth of queries over len(lk)/steps launches
+        lk_bytes = lookup_bytes(ppg, dims) * iters * args.steps // max(1, len(lk))
         ach = lk_bytes / (lk_ms * 1e-3) / 1e9
         traffic = None
         if os.path.exists(PMC_TRAFFIC_FILE):

@@ -74,6 +74,28 @@ def test_train_mode_returns_all_predictions():
     assert torch.equal(preds[-1], up)
 
 
+@pytest.mark.parametrize("lookup", ["joined", "lane"])
+@pytest.mark.parametrize("b", [2, 3, 8])
+def test_pair_lanes_equal_single_lane(lookup, b):
+    """The split update loop on two pair lanes (streams) gives the single-lane results bit for bit (odd batches:
+    ragged halves), in test mode and as the per-iteration prediction list."""
+    img0, img1 = synthetic.synthetic_pair(2, 128, 160, seed=5)
+    reps = -(-b // 2)
+    p0 = img0.repeat(reps, 1, 1, 1)[:b].to(DEV)
+    p1 = img1.repeat(reps, 1, 1, 1)[:b].to(DEV)
+    p1[-1] = torch.roll(p1[-1], 3, dims=-1)  # distinct last pair
+    model = _model(RAFT)
+    outs = {}
+    with torch.inference_mode():
+        for lanes in (1, 2):
+            model.pair_lanes, model.pair_lookup = lanes, lookup
+            outs[lanes] = (model(p0, p1, iters=4, test_mode=True), model(p0, p1, iters=3))
+    (lo1, up1), preds1 = outs[1]
+    (lo2, up2), preds2 = outs[2]
+    assert torch.equal(lo1, lo2) and torch.equal(up1, up2)
+    assert len(preds1) == len(preds2) == 3 and all(torch.equal(a, c) for a, c in zip(preds1, preds2))
+
+
 def test_fused_update_matches_module_update_block():
     """FusedUpdate (fused bias/activation/GRU kernels, merged z|r convolution, persistent [h | x] buffers) against
     the nn.Module update block on the same GPU, two steps so the carried state is checked too."""

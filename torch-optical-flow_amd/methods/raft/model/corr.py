@@ -78,6 +78,7 @@ class CorrBlock:
         self.radius = radius
         self._pyramid: Optional[List[Tensor]] = None
         self._tiled = None
+        self._batch = fmap1.shape[0]
         if torch.is_grad_enabled() and (fmap1.requires_grad or fmap2.requires_grad):
             # training (raft.py:149-175): canonical levels with native backward kernels
             self._pyramid = list(_CorrPyramidFn.apply(fmap1, fmap2, num_levels))
@@ -131,6 +132,19 @@ class CorrBlock:
         for lvl in range(self.num_levels):
             view[..., lvl * ls : lvl * ls + kk] = corr[:, lvl * kk : (lvl + 1) * kk].permute(0, 2, 3, 1)
         return out
+
+    def batch_slice(self, b0: int, b1: int) -> "CorrBlock":
+        """A CorrBlock over the pairs [b0, b1) sharing this one's levels (views, no copy): an addition, used by the RAFT
+        forward to run pair halves on two streams."""
+        view = CorrBlock.__new__(CorrBlock)
+        view.num_levels, view.radius, view._grad = self.num_levels, self.radius, self._grad
+        if self._tiled is not None:
+            view._tiled, view._pyramid = self._tiled.batch_slice(b0, b1), None
+        else:
+            hw = self._pyramid[0].shape[0] // self._batch
+            view._tiled, view._pyramid = None, [t[b0 * hw : b1 * hw] for t in self._pyramid]
+        view._batch = b1 - b0
+        return view
 
     @staticmethod
     def corr(fmap1: Tensor, fmap2: Tensor) -> Tensor:

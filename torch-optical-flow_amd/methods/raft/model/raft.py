@@ -93,6 +93,11 @@ class RAFT(nn.Module):
         # "split": encoders on the split-fp16 kernels (SplitEncoder) in GPU inference; "module": nn.Module (MIOpen)
         self.encoder_impl = "split"
         self.encoder_streams = True  # cnet beside fnet + the corr pyramid (inference, split encoders)
+        # split update loop over >= 2 pairs (CorrBlock): the pairs' two halves run on two streams so that one half's
+        # convolutions fill the CUs the other half's leave idle at a wave tail. pair_lookup "joined": one full-batch
+        # lookup per iteration on the main stream (both halves joined around it); "lane": each half looks up its own.
+        self.pair_lanes = 2
+        self.pair_lookup = "joined"
 
     # -- checkpoints -------------------------------------------------------------------------------------
     @classmethod
@@ -135,6 +140,58 @@ class RAFT(nn.Module):
         up_flow = F.unfold(8 * flow, [3, 3], padding=1).view(n, 2, 9, 1, 1, h, w)
         up_flow = torch.sum(mask * up_flow, dim=2).permute(0, 1, 4, 2, 5, 3)
         return up_flow.reshape(n, 2, 8 * h, 8 * w)
+
+    def _split_update_lanes(self, corr_fn, cnet_out: Tensor, coords0: Tensor, coords1: Tensor, iters: int, hdim: int,
+                            test_mode: bool) -> List[Tensor]:
+        """The split update loop with the pairs in ``pair_lanes`` parts, each on its own stream (lane) with its own side stream;
+        coords1 is advanced in place. Per-pixel results are those of the single-lane loop bit for bit (no reduction
+        crosses pairs). Returns the upsampled flows (test mode: the last one only)."""
+        b = cnet_out.shape[0]
+        dev = cnet_out.device
+        n = min(self.pair_lanes, b)
+        edges = [(b * i) // n for i in range(n + 1)]
+        cuts = list(zip(edges[:-1], edges[1:]))
+        main = torch.cuda.current_stream(dev)
+        lanes = [main] + [_side_stream(dev, 100 + i) for i in range(1, n)]
+        for st in lanes[1:]:
+            st.wait_stream(main)
+        runners = []
+        for i, ((b0, b1), st) in enumerate(zip(cuts, lanes)):
+            with torch.cuda.stream(st):
+                slot = 0 if i == 0 else 200 + i
+                runners.append(SplitUpdate(self.update_block, cnet_out[b0:b1], hdim, side_slot=slot))
+        joined = self.pair_lookup == "joined"
+        hw = cnet_out.shape[2] * cnet_out.shape[3]
+        if joined:
+            rows = torch.empty((b * hw, 32 * runners[0].cgroups), device=dev, dtype=torch.float32)
+            h, w = cnet_out.shape[2:]
+            ins = [_native.F32In(rows[b0 * hw : b1 * hw], b1 - b0, h, w) for b0, b1 in cuts]
+        else:
+            parts = [corr_fn.batch_slice(b0, b1) for b0, b1 in cuts]
+        outs = []
+        for itr in range(iters):
+            last = itr == iters - 1
+            need = not test_mode or last
+            mask = torch.empty((b, 576, *cnet_out.shape[2:]), device=dev, dtype=torch.float32) if need else None
+            if joined:
+                for st in lanes[1:]:
+                    main.wait_stream(st)
+                corr_fn.lookup_nhwc(coords1, rows)
+            if joined or need:  # (need: the mask block may still be in use by earlier main-stream work)
+                for st in lanes[1:]:
+                    st.wait_stream(main)
+            for i, ((b0, b1), st) in enumerate(zip(cuts, lanes)):
+                with torch.cuda.stream(st):
+                    c1 = coords1[b0:b1]
+                    corr_in = ins[i] if joined else runners[i].lookup(parts[i], c1)
+                    runners[i].update(corr_in, c1, need, mask_out=mask[b0:b1] if need else None)
+            if need:
+                for st in lanes[1:]:
+                    main.wait_stream(st)
+                outs.append(self.upsample_flow(coords1 - coords0, mask))
+        for st in lanes[1:]:
+            main.wait_stream(st)
+        return outs
 
     def forward(
         self,
@@ -184,6 +241,12 @@ class RAFT(nn.Module):
         impl = self.update_impl if gpu_inference else "module"
         flow_predictions = []
         flow_up = None
+        if impl == "split" and self.pair_lanes > 1 and cnet_out.shape[0] > 1 and hasattr(corr_fn, "lookup_nhwc"):
+            coords1 = coords1.contiguous()
+            flow_predictions = self._split_update_lanes(corr_fn, cnet_out, coords0, coords1, iters, hdim, test_mode)
+            if test_mode:
+                return coords1 - coords0, flow_predictions[-1]
+            return flow_predictions
         if impl == "split":
             # coords1 is advanced in place by the flow head's epilogue (raft.py:133)
             runner = SplitUpdate(self.update_block, cnet_out, hdim)

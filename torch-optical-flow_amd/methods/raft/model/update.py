@@ -161,8 +161,9 @@ class FusedUpdate:
 _SIDE_STREAMS = {}
 
 
-def _side_stream(device: torch.device) -> "torch.cuda.Stream":
-    key = torch.device(device).index
+def _side_stream(device: torch.device, slot: int = 0) -> "torch.cuda.Stream":
+    """A persistent extra stream per (device, slot), reused across forwards."""
+    key = (torch.device(device).index, slot)
     if key not in _SIDE_STREAMS:
         _SIDE_STREAMS[key] = torch.cuda.Stream(device=device)
     return _SIDE_STREAMS[key]
@@ -189,7 +190,7 @@ class SplitUpdate:
     last iteration the mask head (1x1 conv 256 -> 576 with the x0.25 in its epilogue, fp32 NCHW).
     """
 
-    def __init__(self, block: BasicUpdateBlock, cnet_out: Tensor, hdim: int) -> None:
+    def __init__(self, block: BasicUpdateBlock, cnet_out: Tensor, hdim: int, side_slot: int = 0) -> None:
         b, c, h, w = cnet_out.shape
         enc, gru = block.encoder, block.gru
         cdim = c - hdim
@@ -217,7 +218,7 @@ class SplitUpdate:
         self.w = self._weights(block)
         # side stream for the motion encoder's flow branch (one per device, reused across forwards)
         self.streams = getattr(block, "split_streams", True)
-        self.side_stream = _side_stream(dev) if self.streams else None
+        self.side_stream = _side_stream(dev, side_slot) if self.streams else None
 
     @staticmethod
     def _weights(block: BasicUpdateBlock):
@@ -246,21 +247,33 @@ class SplitUpdate:
         block.__dict__["_split_weights"] = (key, w)
         return w
 
-    def step(self, corr_fn, coords1: Tensor, need_mask: bool) -> Optional[Tensor]:
+    def step(self, corr_fn, coords1: Tensor, need_mask: bool, mask_out: Optional[Tensor] = None) -> Optional[Tensor]:
         """One update (`update.py:150-161` + `raft.py:128-133`): coords1 is advanced IN PLACE by delta_flow.
-        Returns 0.25 * mask (B, 576, H, W) fp32 when ``need_mask``, else None."""
-        V, conv, w = _native.S32Slice, _native.conv_s32, self.w
+        Returns 0.25 * mask (B, 576, H, W) fp32 when ``need_mask`` (written into ``mask_out`` if given), else None."""
+        return self.update(self.lookup(corr_fn, coords1), coords1, need_mask, mask_out)
+
+    def lookup_rows(self, coords1: Tensor) -> Tensor:
+        """The fp32 NHWC lookup buffer [B*H*W, 32*cgroups] (allocated on first use)."""
+        if self.corr_f32 is None:
+            b, h, wd = self.shape
+            self.corr_f32 = torch.empty((b * h * wd, 32 * self.cgroups), device=coords1.device, dtype=torch.float32)
+        return self.corr_f32
+
+    def lookup(self, corr_fn, coords1: Tensor):
+        """The correlation lookup as convc1's input (`raft.py:128`)."""
         b, h, wd = self.shape
         if hasattr(corr_fn, "lookup_nhwc"):  # CorrBlock: fp32 NHWC rows, split while convc1 stages them
-            if self.corr_f32 is None:
-                self.corr_f32 = torch.empty((b * h * wd, 32 * self.cgroups), device=coords1.device, dtype=torch.float32)
-            corr_fn.lookup_nhwc(coords1, self.corr_f32)
-            corr_in = _native.F32In(self.corr_f32, b, h, wd)
-        else:
-            if self.corr is None:
-                self.corr = _native.s32_empty(b, h, wd, self.cgroups, coords1.device, zero=True)
-            corr_fn.lookup_s32(coords1, self.corr)
-            corr_in = V(self.corr)
+            corr_fn.lookup_nhwc(coords1, self.lookup_rows(coords1))
+            return _native.F32In(self.corr_f32, b, h, wd)
+        if self.corr is None:
+            self.corr = _native.s32_empty(b, h, wd, self.cgroups, coords1.device, zero=True)
+        corr_fn.lookup_s32(coords1, self.corr)
+        return _native.S32Slice(self.corr)
+
+    def update(self, corr_in, coords1: Tensor, need_mask: bool, mask_out: Optional[Tensor] = None) -> Optional[Tensor]:
+        """Everything of one update after the lookup; ``corr_in`` is convc1's input (F32In or S32Slice)."""
+        V, conv, w = _native.S32Slice, _native.conv_s32, self.w
+        b, h, wd = self.shape
         # The motion encoder's two branches are independent (update.py:116-121): the flow branch (flow prep, convf1,
         # convf2) runs on a side stream beside the correlation branch (convc1, convc2), both MFMA-latency bound, and
         # joins before the motion conv. The side stream starts after the lookup, which thus runs alone (its bench
@@ -292,7 +305,7 @@ class SplitUpdate:
         conv(V(self.fh), w["fh2"], 32, f32=coords1, f32_accumulate=True)
         if not need_mask:
             return None
-        mask = torch.empty((b, 576, h, wd), device=coords1.device, dtype=torch.float32)
+        mask = mask_out if mask_out is not None else torch.empty((b, 576, h, wd), device=coords1.device, dtype=torch.float32)
         conv(net, w["m1"], 128, "relu", y0=V(self.fh))
         conv(V(self.fh), w["m2"], 64, out_scale=0.25, f32=mask)
         return mask

@@ -262,6 +262,11 @@ class TiledPyramid:
     def __init__(self, levels, dims, queries):
         self.levels, self.dims, self.queries = levels, dims, queries
 
+    def batch_slice(self, b0: int, b1: int) -> "TiledPyramid":
+        """Views of the pairs [b0, b1) (queries are pair-major, so each level's rows are one contiguous range)."""
+        hw = self.dims[0][0] * self.dims[0][1]
+        return TiledPyramid([t[b0 * hw : b1 * hw] for t in self.levels], self.dims, (b1 - b0) * hw)
+
     def untile(self, l: int) -> torch.Tensor:
         """Canonical (B*H*W, 1, H_l, W_l) copy of level l (the reference's corr_pyramid[l]), bit-exact."""
         hl, wl = self.dims[l]
