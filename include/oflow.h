@@ -19,6 +19,8 @@
  *   oflow_conv_s32 & co.    <- methods/raft/model/update.py:40-161 (update-block convolutions)
  *   oflow_stem_patches_s32, oflow_norm_*, oflow_conv_s32_ex <- methods/raft/model/extractor.py:35-231 (encoders)
  *   oflow_convex_upsample_f32 <- methods/raft/model/raft.py:73-85 (RAFT.upsample_flow)
+ *   oflow_flow_stats_f32, oflow_flow2rgb_f32 <- optical_flow/visualization/flow2rgb.py:19-73 (+ visualization/methods/)
+ *   oflow_flow_pack_f32     <- optical_flow/io/middlebury.py:43-71, optical_flow/io/pfm.py:79-104 (file payloads)
  */
 #ifndef OFLOW_H_
 #define OFLOW_H_
@@ -263,6 +265,30 @@ int oflow_corr_lookup_backward_f32(const float* d_grad_out, const float* d_coord
                                    void* stream);
 int oflow_corr_pyramid_grad_combine_f32(float* const* d_grad_levels, const int* level_h, const int* level_w,
                                         int num_levels, long long Q, void* stream);
+
+/*
+ * Inference I/O (csrc/flow_io.hip).
+ * oflow_flow_stats_f32: flow (B, 2, H, W) -> d_partials (B, OFLOW_FLOW_STATS_CHUNKS, 2): per-chunk maxima of |flow|
+ *   and of the flow values, after clip to [clip_lo, clip_hi] (when clip != 0) and y negation (when invert_y != 0).
+ * oflow_flow2rgb_f32: flow (B, 2, H, W) -> d_rgb (B, 3, H, W) in [0, 1], the reference's flow2rgb
+ *   (optical_flow/visualization/flow2rgb.py:19-73). method OFLOW_FLOW2RGB_{BAKER,HSV,MEISTER}. The flow is divided
+ *   by denom (= max_norm + 1e-5, the caller's max_norm) when have_denom != 0, else by max|flow| + 1e-5 taken from
+ *   d_partials (which oflow_flow_stats_f32 must have filled with the same clip / invert_y, earlier on the stream).
+ *   d_partials is also required for MEISTER (its max_flow). Same clip / invert_y semantics as above.
+ * oflow_flow_pack_f32: planar flow (B, 2, H, W) -> per image the file payload (H, W, channels) fp32:
+ *   channels 2 = Middlebury .flo rows (io/middlebury.py:64-71); channels 3 = PFM rows with a zero third channel,
+ *   written bottom row first when flip_rows != 0 (io/pfm.py:95-98). B, H <= 65535.
+ */
+#define OFLOW_FLOW_STATS_CHUNKS 128
+#define OFLOW_FLOW2RGB_BAKER 0
+#define OFLOW_FLOW2RGB_HSV 1
+#define OFLOW_FLOW2RGB_MEISTER 2
+int oflow_flow_stats_f32(const float* d_flow, int B, int H, int W, int clip, float clip_lo, float clip_hi,
+                         int invert_y, float* d_partials, void* stream);
+int oflow_flow2rgb_f32(const float* d_flow, int B, int H, int W, int method, int clip, float clip_lo, float clip_hi,
+                       int invert_y, int have_denom, float denom, const float* d_partials, float* d_rgb, void* stream);
+int oflow_flow_pack_f32(const float* d_flow, int B, int H, int W, int channels, int flip_rows, float* d_out,
+                        void* stream);
 
 #ifdef __cplusplus
 }

@@ -10,7 +10,7 @@ written. Bytecode writing is disabled so the read-only tree stays untouched.
 Inputs come from the repository's own deterministic generators (``model/synthetic.py``), which the GPU box
 re-runs bit-for-bit; fmaps are therefore not stored, only a float64 checksum that the tests re-verify.
 
-Usage:  python tests/golden/gen_goldens.py
+Usage:  python tests/golden/gen_goldens.py [corr] [warp] [raft] [io]   (default: all)
 """
 from __future__ import annotations
 
@@ -181,14 +181,78 @@ def gen_raft(RAFT, InputPadder) -> None:
     np.savez_compressed(os.path.join(HERE, "raft_e2e.npz"), **out)
 
 
+def io_flows():
+    """Flow fields of the I/O goldens, from the repository's own generators (the tests rebuild them)."""
+    flows = {
+        # the reference test's shape (tests/visualization/test_flow2rgb.py:35), hash noise instead of randn
+        "n": torch.from_numpy(synthetic.hash_normal(950, (4, 2, 5, 6), 100.0)),
+        "s": torch.from_numpy(synthetic.hash_normal(951, (2, 2, 37, 53), 6.0)),
+    }
+    # colour-wheel edges: exact axis directions (atan2 = +-pi, +-pi/2, 0: baker's k1 wrap), zero flow, one vector
+    # longer than every other (rad == 1 after normalisation)
+    e = torch.zeros(1, 2, 3, 4)
+    e[0, :, 0, :] = torch.tensor([[-1.0, 1.0, 0.0, 0.0], [0.0, 0.0, -1.0, 1.0]])
+    e[0, :, 1, :] = torch.tensor([[-5.0, 3.0, 0.25, -2.0], [1e-7, -4.0, 7.0, -2.0]])
+    e[0, :, 2, 3] = torch.tensor([12.0, -9.0])
+    flows["e"] = e
+    return flows
+
+
+IO_OPTIONS = (
+    # (tag, clip, max_norm, invert_y)
+    ("d", None, None, False),
+    ("c1", 1.0, None, False),
+    ("c50", 50.0, None, False),
+    ("cpos", (0.0, 50.0), None, False),
+    ("m30", None, 30.0, False),
+    ("inv", None, None, True),
+    ("all", 20.0, 8.0, True),
+)
+
+
+def gen_io() -> None:
+    """flow2rgb / colorwheel (`visualization/flow2rgb.py:19-108`, `methods/*.py`) and the .flo / PFM writers
+    (`io/middlebury.py:43-71`, `io/pfm.py:79-104`): expected RGB fields and file bytes."""
+    from optical_flow.io.middlebury import write_middlebury
+    from optical_flow.io.pfm import write_pfm
+    from optical_flow.visualization.flow2rgb import colorwheel, flow2rgb
+
+    out = {}
+    for name, flow in io_flows().items():
+        out[f"flow_{name}"] = flow.numpy()
+        for method in ("baker", "hsv", "meister"):
+            for tag, clip, max_norm, inv in IO_OPTIONS:
+                if name == "e" and tag not in ("d", "inv", "m30"):
+                    continue
+                out[f"rgb_{name}_{method}_{tag}"] = flow2rgb(flow, method, clip, max_norm, inv).numpy()
+    for method in ("baker", "hsv", "meister"):
+        out[f"wheel_{method}"] = colorwheel(method, size=48).numpy()
+    import tempfile
+
+    with tempfile.TemporaryDirectory() as d:
+        f = io_flows()["s"][1]
+        for fmt, fn in (("flo", write_middlebury), ("pfm", write_pfm)):
+            path = os.path.join(d, "x." + fmt)
+            fn(path, f)
+            with open(path, "rb") as fh:
+                out[f"bytes_{fmt}"] = np.frombuffer(fh.read(), dtype=np.uint8)
+    np.savez_compressed(os.path.join(HERE, "io_small.npz"), **out)
+
+
 def main() -> int:
     if not os.path.isdir(REF):
         print("gen_goldens: /root/reference absent; fixtures are committed, nothing to do")
         return 0
     RAFT, CorrBlock, InputPadder, bilinear_sampler, coords_grid, ref_operator = _import_reference()
-    gen_corr(CorrBlock, coords_grid)
-    gen_warp(ref_operator)
-    gen_raft(RAFT, InputPadder)
+    which = sys.argv[1:] or ["corr", "warp", "raft", "io"]
+    if "corr" in which:
+        gen_corr(CorrBlock, coords_grid)
+    if "warp" in which:
+        gen_warp(ref_operator)
+    if "raft" in which:
+        gen_raft(RAFT, InputPadder)
+    if "io" in which:
+        gen_io()
     return 0
 
 

@@ -149,9 +149,9 @@ class SplitEncoder:
             raise RuntimeError("SplitEncoder: batch norm needs eval mode (running statistics)")
         self.enc = enc
         self.inorm = enc.norm_fn == "instance"
-        key = tuple((q.data_ptr(), q._version) for q in enc.parameters()) + tuple(
-            (q.data_ptr(), q._version) for q in enc.buffers()
-        )
+        from .update import tensor_key
+
+        key = tuple(tensor_key(q) for q in enc.parameters()) + tuple(tensor_key(q) for q in enc.buffers())
         cache = enc.__dict__.get("_split_weights")
         if cache is None or cache[0] != key:
             enc.__dict__["_split_weights"] = (key, self._pack(enc))

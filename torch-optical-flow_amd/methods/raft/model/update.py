@@ -169,8 +169,15 @@ def _side_stream(device: torch.device, slot: int = 0) -> "torch.cuda.Stream":
     return _SIDE_STREAMS[key]
 
 
+def tensor_key(q: Tensor):
+    """(storage, version) of a weight for the packed-weight caches. Tensors created under torch.inference_mode()
+    (e.g. a model built inside an inference-mode function, as predict.py:39 does) have no version counter: they are
+    keyed by storage alone."""
+    return (q.data_ptr(), -1 if q.is_inference() else q._version)
+
+
 def _weights_key(block: nn.Module):
-    return tuple((q.data_ptr(), q._version) for q in block.parameters())
+    return tuple(tensor_key(q) for q in block.parameters())
 
 
 class SplitUpdate:

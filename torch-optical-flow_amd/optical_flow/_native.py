@@ -57,6 +57,9 @@ SYMBOLS = (
     "oflow_corr_lookup_tiled_nhwc_f32",
     "oflow_corr_lookup_backward_f32",
     "oflow_corr_pyramid_grad_combine_f32",
+    "oflow_flow_stats_f32",
+    "oflow_flow2rgb_f32",
+    "oflow_flow_pack_f32",
 )
 
 _lib = None
@@ -175,6 +178,12 @@ def load() -> ctypes.CDLL:
     lib.oflow_corr_lookup_tiled_nhwc_f32.argtypes = [PP, IP, IP, I, P, I, I, I, I, P, I, P]
     lib.oflow_convex_upsample_f32.restype = I
     lib.oflow_convex_upsample_f32.argtypes = [P, P, I, I, I, P, P]
+    lib.oflow_flow_stats_f32.restype = I
+    lib.oflow_flow_stats_f32.argtypes = [P, I, I, I, I, F, F, I, P, P]
+    lib.oflow_flow2rgb_f32.restype = I
+    lib.oflow_flow2rgb_f32.argtypes = [P, I, I, I, I, I, F, F, I, I, F, P, P, P]
+    lib.oflow_flow_pack_f32.restype = I
+    lib.oflow_flow_pack_f32.argtypes = [P, I, I, I, I, I, P, P]
     v = lib.oflow_abi_version()
     if v != ABI_VERSION:
         raise RuntimeError(f"liboflow_hip.so ABI version {v}, expected {ABI_VERSION}: rebuild the library")
@@ -424,6 +433,65 @@ def convex_upsample(flow: torch.Tensor, mask: torch.Tensor) -> torch.Tensor:
         return out
     with torch.cuda.device(fl.device), _Timed("upsample_flow", fl.device):
         _check(load().oflow_convex_upsample_f32(fl.data_ptr(), mk.data_ptr(), b, h, w, out.data_ptr(), _stream(fl.device)), what)
+    return out
+
+
+FLOW2RGB_METHODS = {"baker": 0, "hsv": 1, "meister": 2}
+FLOW_STATS_CHUNKS = 128  # include/oflow.h OFLOW_FLOW_STATS_CHUNKS
+
+
+def _flow_b2hw(flow: torch.Tensor, what: str) -> torch.Tensor:
+    fl = _gpu_f32(flow, "flow", what)
+    if fl.dim() != 4 or fl.shape[1] != 2:
+        raise RuntimeError(f"{what}: flow {tuple(flow.shape)} must be (B, 2, H, W)")
+    return fl
+
+
+def flow2rgb(flow: torch.Tensor, method: str, clip, denom, invert_y: bool) -> torch.Tensor:
+    """optical_flow.flow2rgb (optical_flow/visualization/flow2rgb.py:19-73) on (B, 2, H, W) fp32: clip (None or a
+    (lo, hi) pair), y inversion, division by ``denom`` (the fp32 value of max_norm + 1e-5; None = per image
+    max |flow| + 1e-5) and the baker / hsv / meister colour map, in two launches (flow_stats, flow2rgb) ->
+    (B, 3, H, W) fp32."""
+    what = "flow2rgb"
+    if method not in FLOW2RGB_METHODS:
+        raise ValueError(f"Unknown method: '{method}'.")
+    fl = _flow_b2hw(flow, what)
+    b, _, h, w = fl.shape
+    out = torch.empty((b, 3, h, w), device=fl.device, dtype=torch.float32)
+    if out.numel() == 0:
+        return out
+    do_clip = clip is not None
+    lo, hi = (float(clip[0]), float(clip[1])) if do_clip else (0.0, 0.0)
+    have_denom = denom is not None
+    denom = float(denom) if have_denom else 0.0
+    need_stats = (not have_denom) or method == "meister"
+    lib = load()
+    with torch.cuda.device(fl.device), _Timed("flow2rgb", fl.device):
+        stream = _stream(fl.device)
+        parts = None
+        if need_stats:
+            parts = torch.empty((b, FLOW_STATS_CHUNKS, 2), device=fl.device, dtype=torch.float32)
+            _check(lib.oflow_flow_stats_f32(fl.data_ptr(), b, h, w, int(do_clip), lo, hi, int(bool(invert_y)),
+                                            parts.data_ptr(), stream), what)
+        _check(lib.oflow_flow2rgb_f32(fl.data_ptr(), b, h, w, FLOW2RGB_METHODS[method], int(do_clip), lo, hi,
+                                      int(bool(invert_y)), int(have_denom), denom,
+                                      parts.data_ptr() if parts is not None else None, out.data_ptr(), stream), what)
+    return out
+
+
+def flow_pack(flow: torch.Tensor, channels: int, flip_rows: bool) -> torch.Tensor:
+    """Planar (B, 2, H, W) flow -> the file payload (B, H, W, channels) fp32 on the device: channels 2 = Middlebury
+    .flo rows (optical_flow/io/middlebury.py:64-71), 3 = PFM rows (zero third channel, bottom-up when flip_rows;
+    optical_flow/io/pfm.py:95-98)."""
+    what = "flow_pack"
+    fl = _flow_b2hw(flow, what)
+    b, _, h, w = fl.shape
+    out = torch.empty((b, h, w, channels), device=fl.device, dtype=torch.float32)
+    if out.numel() == 0:
+        return out
+    with torch.cuda.device(fl.device), _Timed("flow_pack", fl.device):
+        _check(load().oflow_flow_pack_f32(fl.data_ptr(), b, h, w, int(channels), int(bool(flip_rows)),
+                                          out.data_ptr(), _stream(fl.device)), what)
     return out
 
 
