@@ -173,8 +173,6 @@ int oflow_gru_blend_f32(const float* d_zr, long long szr, const float* d_bz, con
  * oflow_flow_prep_s32: flow = coords1 - pixel grid (raft.py:129) as the 7x7 patch matrix of convf1
  *   (d_patches: S32 with 4 groups; channel t*2 + c = flow c at tap t = ky*7 + kx, zero padded) and, if not NULL,
  *   the 2 flow channels at d_flow0 / d_flow1 (byte address of the hi half of the x channel; y follows).
- * oflow_corr_lookup_tiled_s32: oflow_corr_lookup_tiled_f32 written as S32 (d_out, out_pixel_stride bytes) with
- *   level l at channels [l*LS, l*LS + (2r+1)^2), LS = (2r+1)^2 rounded up to 8, zeros in the LS - (2r+1)^2 after it.
  */
 int oflow_conv_s32(const void* d_x, long long x_pixel_stride, int in_groups, const void* d_wpack, int n_pad,
                    const float* d_wscale, const float* d_bias, int N, int B, int H, int W, int kh, int kw, int block_n,
@@ -186,16 +184,14 @@ int oflow_pack_s32_f32(const float* d_x, long long x_batch_stride, int C, int B,
                        float* d_nhwc, int nhwc_pixel_stride, void* stream);
 int oflow_flow_prep_s32(const float* d_coords, int B, int H, int W, void* d_patches, void* d_flow0,
                         long long flow0_pixel_stride, void* d_flow1, long long flow1_pixel_stride, void* stream);
-/* oflow_corr_lookup_tiled_nhwc_f32: the tiled lookup as fp32 NHWC rows [B*H*W][row_floats] for the RAFT forward's convc1
- * (oflow_conv_s32_ex2, OFLOW_IN_F32): level l at channels [l*LS, l*LS + (2r+1)^2), LS = (2r+1)^2 rounded up to 8, every
- * other channel of the row written as 0; row_floats >= num_levels*LS, a multiple of 32. Same values as
- * oflow_corr_lookup_tiled_f32. Replaces corr.py:56-77 + the channel concat feeding update.py:120-121. */
+/* oflow_corr_lookup_tiled_nhwc_f32: the tiled lookup as fp32 NHWC rows [B*H*W][row_floats] (d_out 16-B aligned) in the
+ * reference's channel order: row q, channel l*(2r+1)^2 + k = oflow_corr_lookup_tiled_f32's (b, l*(2r+1)^2 + k, y, x) bit for
+ * bit; row_floats >= num_levels*(2r+1)^2, channels past that are not written. With row_floats = num_levels*(2r+1)^2 (324)
+ * it is the RAFT forward's convc1 input (oflow_conv_s32_ex2, OFLOW_IN_F32). Replaces corr.py:56-77 + the permute feeding
+ * update.py:120-121. */
 int oflow_corr_lookup_tiled_nhwc_f32(const float* const* d_levels, const int* level_h, const int* level_w, int num_levels,
                                      const float* d_coords, int B, int H, int W, int radius, float* d_out, int row_floats,
                                      void* stream);
-int oflow_corr_lookup_tiled_s32(const float* const* d_levels, const int* level_h, const int* level_w, int num_levels,
-                                const float* d_coords, int B, int H, int W, int radius, void* d_out,
-                                long long out_pixel_stride, void* stream);
 
 /*
  * Encoders on the split-fp16 path (methods/raft/model/extractor.py:35-231; csrc/encoder_s32.hip).
@@ -213,8 +209,9 @@ int oflow_corr_lookup_tiled_s32(const float* const* d_levels, const int* level_h
  *   NHWC output [P][in_groups*32] of the previous convolution (x_pixel_stride = in_groups*128), normalised and ReLU'd
  *   while staged, x = max(0, raw * d_in_scale[b, c] + d_in_shift[b, c]) ([B][in_groups*32] each) -- the instance
  *   norm + ReLU between a residual block's two 3x3 convs (extractor.py:75-76) never materialises (3x3, epilogue 0,
- *   in_groups <= 4); OFLOW_IN_F32: a dense fp32 NHWC input split into hi + lo while staged (1x1, epilogue 0,
- *   block_n 128: convc1 reading oflow_corr_lookup_tiled_nhwc_f32's output).
+ *   in_groups <= 4); OFLOW_IN_F32: an fp32 NHWC input of cin = x_pixel_stride/4 channels per pixel
+ *   ((in_groups-1)*32 < cin <= in_groups*32, x_pixel_stride % 16 == 0; channels past cin stage as zeros) split into
+ *   hi + lo while staged (1x1, epilogue 0, block_n 128: convc1 reading oflow_corr_lookup_tiled_nhwc_f32's rows).
  * oflow_stem_patches_s32: 7x7/2 pad-3 patch matrix of a (B, C, H, W) fp32 image: S32 (B, ceil(H/2), ceil(W/2),
  *   out_groups) with channel t*C + c (t = ky*7 + kx), zeros past 49*C.
  * oflow_norm_stats_finalize: merge the partials (fp64 sums) -> alpha = 1/sqrt(var + eps), beta = -mean * alpha, [B][C].

@@ -183,28 +183,6 @@ def test_pack_s32_and_flow_prep():
         assert float((N.s32_to_f32(t)[:, 382:] - flow).abs().max()) <= 1e-6 * float(flow.abs().max())
 
 
-@pytest.mark.parametrize("sigma", [0.0, 3.0, 25.0])
-def test_lookup_s32_equals_lookup(sigma):
-    g = torch.Generator().manual_seed(int(sigma) + 1)
-    b, c, h, w = 2, 256, 23, 37
-    f1 = torch.randn(b, c, h, w, generator=g).to(DEV)
-    f2 = torch.randn(b, c, h, w, generator=g).to(DEV)
-    pyr = N.corr_pyramid_tiled(f1, f2, 4)
-    coords = coords_grid(b, h, w, device=DEV) + torch.randn(b, 2, h, w, generator=g).to(DEV) * sigma
-    ref = N.corr_lookup_tiled(pyr, coords, 4)
-    out = N.s32_empty(b, h, w, 11, DEV, zero=True)
-    N.corr_lookup_tiled_s32(pyr, coords, 4, out)
-    got = N.s32_to_f32(out)
-    perm = N.lookup_s32_perm(4, 4).to(DEV)
-    assert N.lookup_s32_stride(4) == 88 and perm.numel() == 352
-    real = perm >= 0
-    assert float((got[:, real] - ref[:, perm[real]]).abs().max()) <= 2.0 ** -21 * max(1.0, float(ref.abs().max()))
-    assert bool((got[:, ~real] == 0).all())
-    # the fp32 -> S32 repacking used by the materialised / on-the-fly paths gives the same layout
-    out2 = N.pack_lookup_s32(ref, 4, 4, N.s32_empty(b, h, w, 11, DEV, zero=True))
-    assert torch.equal(out2, out)
-
-
 @pytest.mark.parametrize("c,n,bn", [(64, 64, 64), (96, 96, 96), (128, 128, 128)])
 def test_conv_normalise_on_load_equals_norm_apply(c, n, bn):
     """oflow_conv_s32_ex2 with a raw fp32 NHWC input normalised + ReLU'd while staged (NhwcNormIn) equals the
@@ -228,10 +206,12 @@ def test_conv_normalise_on_load_equals_norm_apply(c, n, bn):
 
 
 @pytest.mark.parametrize("sigma", [0.0, 3.0, 25.0])
-@pytest.mark.parametrize("radius,levels", [(4, 4), (2, 3), (3, 5)])
-def test_lookup_nhwc_equals_lookup(sigma, radius, levels):
-    """oflow_corr_lookup_tiled_nhwc_f32 (the RAFT forward's lookup, query-major workgroups) = the NCHW lookup
-    bit-for-bit in the permuted channel order, zeros in every other channel of the row; ragged last workgroup."""
+@pytest.mark.parametrize("radius,levels", [(4, 4), (2, 3), (3, 5), (7, 2)])
+@pytest.mark.parametrize("pad", [0, 12])
+def test_lookup_nhwc_equals_lookup(sigma, radius, levels, pad):
+    """oflow_corr_lookup_tiled_nhwc_f32 (the RAFT forward's lookup: segment-DMA gathers, query-major waves) = the
+    NCHW lookup permuted to NHWC, bit for bit; row pitch = L*K*K (dense, float4 stores) or padded (scalar stores, the
+    pad channels untouched); ragged last wave (33*37*2 queries)."""
     g = torch.Generator().manual_seed(int(sigma) + 7 * radius)
     b, c, h, w = 2, 256, 33, 37
     f1 = torch.randn(b, c, h, w, generator=g).to(DEV)
@@ -239,21 +219,20 @@ def test_lookup_nhwc_equals_lookup(sigma, radius, levels):
     pyr = N.corr_pyramid_tiled(f1, f2, levels)
     coords = coords_grid(b, h, w, device=DEV) + torch.randn(b, 2, h, w, generator=g).to(DEV) * sigma
     ref = N.corr_lookup_tiled(pyr, coords, radius)  # (B, L*K*K, H, W)
-    ls, kk = N.lookup_s32_stride(radius), (2 * radius + 1) ** 2
-    row = ((levels * ls + 31) // 32) * 32
-    out = torch.full((b * h * w, row), 7.0, device=DEV)
+    ch = levels * (2 * radius + 1) ** 2
+    out = torch.full((b * h * w, ch + pad), 7.0, device=DEV)
     N.corr_lookup_tiled_nhwc(pyr, coords, radius, out)
-    got = out.view(b, h, w, row)
-    expect = torch.zeros_like(got)
-    for lvl in range(levels):
-        expect[..., lvl * ls : lvl * ls + kk] = ref[:, lvl * kk : (lvl + 1) * kk].permute(0, 2, 3, 1)
-    assert torch.equal(got, expect)
+    got = out.view(b, h, w, ch + pad)
+    assert torch.equal(got[..., :ch], ref.permute(0, 2, 3, 1))
+    assert bool((got[..., ch:] == 7.0).all())
 
 
-def test_conv_f32_input_equals_s32_input():
-    """convc1 reading the fp32 NHWC lookup rows (F32In, split while staged) = reading the same values as S32."""
+@pytest.mark.parametrize("c", [352, 324, 100])
+def test_conv_f32_input_equals_s32_input(c):
+    """convc1 reading fp32 NHWC rows (F32In, split while staged; rows of C floats, channels past C staged as zeros,
+    C = 324 is the lookup row) = reading the same values as S32."""
     g = torch.Generator().manual_seed(3)
-    b, h, w, c, n = 2, 23, 45, 352, 256
+    b, h, w, n = 2, 23, 45, 256
     x = (torch.randn(b * h * w, c, generator=g) * 4).to(DEV)
     s32 = N.s32_from_f32(x.view(b, h, w, c).permute(0, 3, 1, 2).contiguous())
     wt = (torch.randn(n, c, 1, 1, generator=g) * 0.05).to(DEV)

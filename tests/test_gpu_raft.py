@@ -120,15 +120,15 @@ def test_fused_update_matches_module_update_block():
 
 
 class _FixedCorr:
-    """Stands in for CorrBlock: hands the given lookup outputs to SplitUpdate (as S32) in order."""
+    """Stands in for CorrBlock: hands the given lookup outputs to SplitUpdate (as NHWC rows) in order."""
 
     def __init__(self, corrs):
         self.corrs = list(corrs)
 
-    def lookup_s32(self, coords, out):
-        from optical_flow import _native
-
-        return _native.pack_lookup_s32(self.corrs.pop(0), 4, 4, out)
+    def lookup_nhwc(self, coords, out):
+        b, _, h, w = coords.shape
+        out.view(b, h, w, -1).copy_(self.corrs.pop(0).permute(0, 2, 3, 1))
+        return out
 
 
 def test_split_update_matches_module_update_block():

@@ -105,20 +105,16 @@ def main():
     if args.no_lookup:
         print(json.dumps(out, indent=1))
         return
-    # S32 lookup (and the NCHW one) on a real pyramid
+    # the lookup (NHWC rows and NCHW) on a real pyramid
     f1, f2 = synthetic.synthetic_fmaps(b, 256, h, w, stream=3)
     f1, f2 = f1.to(dev), f2.to(dev)
     coords = (coords_grid(b, h, w) + torch.from_numpy(synthetic.hash_normal(4, (b, 2, h, w), 4.0))).to(dev)
     tp = N.corr_pyramid_tiled(f1, f2, 4)
     dims = tp.dims
-    lo = N.s32_empty(b, h, w, 11, dev, zero=True)
-    ls = timed(lambda: N.corr_lookup_tiled_s32(tp, coords, 4, lo), args.iters * 3)
-    lf = torch.empty((b * h * w, 352), device=dev)
+    lf = torch.empty((b * h * w, 324), device=dev)
     lnh = timed(lambda: N.corr_lookup_tiled_nhwc(tp, coords, 4, lf), args.iters * 3)
     ln = timed(lambda: N.corr_lookup_tiled(tp, coords, 4), args.iters * 3)
     lb = lookup_bytes(b, dims)
-    out["lookup_s32_us"] = round(ls * 1e3, 1)
-    out["lookup_s32_GBs"] = round(lb / ls / 1e6, 1)
     out["lookup_nhwc_us"] = round(lnh * 1e3, 1)
     out["lookup_nhwc_GBs"] = round(lb / lnh / 1e6, 1)
     out["lookup_nchw_us"] = round(ln * 1e3, 1)

@@ -72,6 +72,7 @@ struct ConvArgs {
   const float* ia;
   const float* ib;
   int ain;                 // input format: kInS32 / kInF32Norm / kInF32
+  int cin;                 // kInF32: real input channels (row pitch cin * 4 B); channels >= cin stage as zeros
 };
 // input formats of oflow_conv_s32_ex2
 constexpr int kInS32 = OFLOW_IN_S32, kInF32Norm = OFLOW_IN_F32_NORM, kInF32 = OFLOW_IN_F32;
@@ -172,6 +173,7 @@ __global__ __launch_bounds__(kThreads, (VAR & 4) ? 3 : 2) void conv_s32_kernel(C
   // vmcnt precisely instead of draining the queue: halo pixels outside the image load a clamped in-image pixel and
   // are zeroed when written to LDS (the in/out mask and the per-item offsets do not depend on the group).
   long long aoff[APER];
+  int acol[APER];  // kInF32: byte offset of the item's 4 channels within a 32-channel group (added per group, clamped)
   unsigned aok = 0u;
 #pragma unroll
   for (int s_ = 0; s_ < APER; ++s_) {
@@ -180,12 +182,17 @@ __global__ __launch_bounds__(kThreads, (VAR & 4) ? 3 : 2) void conv_s32_kernel(C
     const int gy = ty0 - PH + p / HX, gx = tx0 - PW + p % HX;
     const bool ok = static_cast<unsigned>(gy) < static_cast<unsigned>(a.H) && static_cast<unsigned>(gx) < static_cast<unsigned>(a.W);
     const int cy = min(max(gy, 0), a.H - 1), cx = min(max(gx, 0), a.W - 1);
-    aoff[s_] = (pix0 + (long long)cy * a.W + cx) * a.xps + c * 16;
+    aoff[s_] = (pix0 + (long long)cy * a.W + cx) * a.xps + (AIN == kInF32 ? 0 : c * 16);
+    acol[s_] = c * 16;
     aok |= (ok ? 1u : 0u) << s_;
   }
 #define OFLOW_LOAD_A(RA, G)                                                                                          \
-  _Pragma("unroll") for (int s_ = 0; s_ < APER; ++s_)                                                                \
-    RA[s_] = *reinterpret_cast<const u32x4*>(a.x + aoff[s_] + (long long)(G) * 128);
+  _Pragma("unroll") for (int s_ = 0; s_ < APER; ++s_) {                                                              \
+    if constexpr (AIN == kInF32) /* rows of cin floats: channels past cin re-read the row's last 16 B (zeroed) */   \
+      RA[s_] = *reinterpret_cast<const u32x4*>(a.x + aoff[s_] + min((G) * 128 + acol[s_], a.cin * 4 - 16));        \
+    else                                                                                                             \
+      RA[s_] = *reinterpret_cast<const u32x4*>(a.x + aoff[s_] + (long long)(G) * 128);                              \
+  }
 #define OFLOW_WRITE_A(RA, BUF, G)                                                                                    \
   _Pragma("unroll") for (int s_ = 0; s_ < APER; ++s_) {                                                              \
     const int item = tid + s_ * kThreads;                                                                            \
@@ -195,7 +202,7 @@ __global__ __launch_bounds__(kThreads, (VAR & 4) ? 3 : 2) void conv_s32_kernel(C
         /* 4 fp32 channels (G*32 + 4c ..) [-> relu(x * scale + shift)] -> 4 hi + 4 lo halves (8 B each) */           \
         typedef _Float16 half4_ __attribute__((ext_vector_type(4)));                                                 \
         half4_ h4 = {0, 0, 0, 0}, l4 = {0, 0, 0, 0};                                                                 \
-        if ((aok >> s_) & 1u) {                                                                                      \
+        if (((aok >> s_) & 1u) && (AIN != kInF32 || (G) * 32 + 4 * c < a.cin)) {                                    \
           const float* fv = reinterpret_cast<const float*>(&RA[s_]);                                                 \
           _Pragma("unroll") for (int e_ = 0; e_ < 4; ++e_) {                                                         \
             float v_ = fv[e_];                                                                                       \
@@ -674,7 +681,7 @@ int build_conv_args(ConvArgs& a, const void* d_x, long long x_pixel_stride, int 
   if (B <= 0 || H <= 0 || W <= 0 || N <= 0 || in_groups <= 0 || n_pad < N || n_pad % block_n) return OFLOW_E_SHAPE;
   if (activation < 0 || activation > 3 || res_activation < 0 || res_activation > 3 || epilogue < 0 || epilogue > 2)
     return OFLOW_E_MODE;
-  if ((x_pixel_stride & 127) || ((uintptr_t)d_x & 15) || ((uintptr_t)d_wpack & 15)) return OFLOW_E_ALIGN;
+  if ((x_pixel_stride & 15) || ((uintptr_t)d_x & 15) || ((uintptr_t)d_wpack & 15)) return OFLOW_E_ALIGN;
   if (epilogue == 0 && !d_y0 && !d_f32 && !d_nhwc && !d_stats) return OFLOW_E_NULL;
   if (epilogue != 0 && (!d_y0 || !d_gru_h || !d_gru_z || gru_channels <= 0 || gru_channels % 8)) return OFLOW_E_NULL;
   if (epilogue == 1 && N != 2 * gru_channels) return OFLOW_E_SHAPE;
@@ -720,6 +727,7 @@ int build_conv_args(ConvArgs& a, const void* d_x, long long x_pixel_stride, int 
   a.resps = res_pixel_stride;
   a.res_act = res_activation;
   a.s2d = s2d;
+  a.cin = in_groups * 32;
   (void)kh;
   (void)kw;
   (void)block_n;
@@ -748,7 +756,13 @@ extern "C" int oflow_conv_s32_ex2(const void* d_x, long long x_pixel_stride, int
                                  res_activation, s2d);
   if (st != OFLOW_OK) return st;
   if (in_format < kInS32 || in_format > kInF32) return OFLOW_E_MODE;
-  if (in_format != kInS32 && x_pixel_stride != (long long)in_groups * 128) return OFLOW_E_SHAPE;  // dense [P][kg*32]
+  if (in_format != kInF32 && (x_pixel_stride & 127)) return OFLOW_E_ALIGN;  // S32 / dense fp32: whole 128-B groups
+  if (in_format == kInF32Norm && x_pixel_stride != (long long)in_groups * 128) return OFLOW_E_SHAPE;  // dense [P][kg*32]
+  if (in_format == kInF32) {  // rows of cin fp32 channels, (kg - 1) * 32 < cin <= kg * 32, cin % 4 == 0
+    const long long cin = x_pixel_stride / 4;
+    if ((x_pixel_stride & 15) || cin > (long long)in_groups * 32 || cin <= (long long)(in_groups - 1) * 32) return OFLOW_E_SHAPE;
+    a.cin = static_cast<int>(cin);
+  }
   if (in_format == kInF32Norm) {  // normalised + ReLU'd on load
     if (!d_in_scale || !d_in_shift) return OFLOW_E_NULL;
     if (kh != 3 || kw != 3 || epilogue != 0 || in_groups > kAinGroups) return OFLOW_E_MODE;

@@ -109,28 +109,13 @@ class CorrBlock:
             return _CorrLookupFn.apply(coords.detach(), self.radius, *self._pyramid)
         return _native.corr_lookup(self._pyramid, coords, self.radius)
 
-    def lookup_s32(self, coords: Tensor, out: Tensor) -> Tensor:
-        """The lookup written as split-fp16 NHWC (S32) into ``out`` for the update block's convc1 (an addition):
-        level l at channels [l*LS, l*LS + (2r+1)^2), LS = ``_native.lookup_s32_stride(r)``; values equal
-        ``__call__``'s up to the fp16 hi/lo representation (22 significant bits)."""
-        if self._tiled is not None:
-            return _native.corr_lookup_tiled_s32(self._tiled, coords, self.radius, out)
-        corr = _native.corr_lookup(self._pyramid, coords, self.radius)
-        return _native.pack_lookup_s32(corr, self.num_levels, self.radius, out)
-
     def lookup_nhwc(self, coords: Tensor, out: Tensor) -> Tensor:
-        """The lookup as fp32 NHWC rows [B*H*W, row] in the S32 layout's channel order (an addition; the RAFT forward's
-        convc1 input): exactly ``__call__``'s values, zeros in the padding channels."""
+        """The lookup as fp32 NHWC rows into ``out`` [B*H*W, L*(2r+1)^2] (an addition; the RAFT forward's convc1
+        input): ``__call__(coords).permute(0, 2, 3, 1)`` written directly by the kernel, bit for bit."""
         if self._tiled is not None:
             return _native.corr_lookup_tiled_nhwc(self._tiled, coords, self.radius, out)
         b, _, h, w = coords.shape
-        corr = _native.corr_lookup(self._pyramid, coords, self.radius)  # (B, L*K*K, H, W)
-        kk = (2 * self.radius + 1) ** 2
-        ls = _native.lookup_s32_stride(self.radius)
-        view = out.view(b, h, w, -1)
-        view.zero_()
-        for lvl in range(self.num_levels):
-            view[..., lvl * ls : lvl * ls + kk] = corr[:, lvl * kk : (lvl + 1) * kk].permute(0, 2, 3, 1)
+        out.view(b, h, w, -1).copy_(_native.corr_lookup(self._pyramid, coords, self.radius).permute(0, 2, 3, 1))
         return out
 
     def batch_slice(self, b0: int, b1: int) -> "CorrBlock":
@@ -170,6 +155,8 @@ class AlternateCorrBlock:
     def __call__(self, coords: Tensor) -> Tensor:
         return _native.corr_lookup_otf(self.fmap1_f16, self.fmap2_pyramid_f16, coords, self.radius)
 
-    def lookup_s32(self, coords: Tensor, out: Tensor) -> Tensor:
-        """``__call__`` repacked as split-fp16 NHWC (S32, ``_native.lookup_s32_stride`` layout) into ``out``."""
-        return _native.pack_lookup_s32(self(coords), self.num_levels, self.radius, out)
+    def lookup_nhwc(self, coords: Tensor, out: Tensor) -> Tensor:
+        """``__call__`` as fp32 NHWC rows [B*H*W, L*(2r+1)^2] into ``out`` (convc1's input)."""
+        b, _, h, w = coords.shape
+        out.view(b, h, w, -1).copy_(self(coords).permute(0, 2, 3, 1))
+        return out

@@ -163,7 +163,7 @@ class RAFT(nn.Module):
         joined = self.pair_lookup == "joined"
         hw = cnet_out.shape[2] * cnet_out.shape[3]
         if joined:
-            rows = torch.empty((b * hw, 32 * runners[0].cgroups), device=dev, dtype=torch.float32)
+            rows = torch.empty((b * hw, runners[0].corr_ch), device=dev, dtype=torch.float32)
             h, w = cnet_out.shape[2:]
             ins = [_native.F32In(rows[b0 * hw : b1 * hw], b1 - b0, h, w) for b0, b1 in cuts]
         else:

@@ -1,8 +1,11 @@
 """GRU update block (reference: methods/raft/model/update.py:40-161).
 
-Consumes the lookup output (B, L*(2r+1)^2, H, W) through ``encoder.convc1``. Convolutions run on
-PyTorch-ROCm (MIOpen); fusing the lookup into ``convc1`` is SURVEY §8(f) row 1 (next). Parameter names equal
-the reference's. ``ConvGRU`` (unused by RAFT) is not provided.
+The ``nn.Module`` classes restate the reference's layers (same parameter names, so checkpoints load); they are
+what autograd / CPU runs use. GPU inference runs ``SplitUpdate``: every convolution on the split-fp16 matrix-core
+kernel (csrc/conv_s32.hip) with the GRU gates, activations, concatenations and the coords update fused into
+convolution epilogues; convc1 reads the lookup's fp32 NHWC rows directly (split into hi + lo while staged).
+``FusedUpdate`` (MIOpen convolutions + fused elementwise kernels) is kept for A/B runs. ``ConvGRU`` (unused by RAFT)
+is not provided.
 """
 from __future__ import annotations
 
@@ -209,9 +212,8 @@ class SplitUpdate:
         self.hx = S(b, h, w, 12, dev)
         self.rhx = S(b, h, w, 12, dev)
         levels, radius = block.corr_levels, block.corr_radius
-        self.cgroups = (levels * _native.lookup_s32_stride(radius) + 31) // 32
-        self.corr = None  # S32 lookup (AlternateCorrBlock), allocated on first use
-        self.corr_f32 = None  # fp32 NHWC lookup rows (CorrBlock), allocated on first use
+        self.corr_ch = levels * (2 * radius + 1) ** 2  # convc1's input: fp32 NHWC lookup rows in the reference order
+        self.corr_f32 = None  # [B*H*W, corr_ch], allocated on first use
         self.c1 = S(b, h, w, 8, dev)
         self.cf = S(b, h, w, 8, dev)
         self.pm = S(b, h, w, 4, dev)
@@ -236,8 +238,7 @@ class SplitUpdate:
         enc, gru, fh = block.encoder, block.gru, block.flow_head
         CW = _native.ConvWeights
         w = {
-            "c1": CW(enc.convc1.weight, enc.convc1.bias, 256,
-                     in_perm=_native.lookup_s32_perm(block.corr_levels, block.corr_radius)),
+            "c1": CW(enc.convc1.weight, enc.convc1.bias, 256),
             "c2": CW(enc.convc2.weight, enc.convc2.bias, 192),
             "f1": CW(enc.convf1.weight, enc.convf1.bias, 128, patches=True),
             "f2": CW(enc.convf2.weight, enc.convf2.bias, 64),
@@ -260,25 +261,20 @@ class SplitUpdate:
         return self.update(self.lookup(corr_fn, coords1), coords1, need_mask, mask_out)
 
     def lookup_rows(self, coords1: Tensor) -> Tensor:
-        """The fp32 NHWC lookup buffer [B*H*W, 32*cgroups] (allocated on first use)."""
+        """The fp32 NHWC lookup buffer [B*H*W, L*(2r+1)^2] (allocated on first use)."""
         if self.corr_f32 is None:
             b, h, wd = self.shape
-            self.corr_f32 = torch.empty((b * h * wd, 32 * self.cgroups), device=coords1.device, dtype=torch.float32)
+            self.corr_f32 = torch.empty((b * h * wd, self.corr_ch), device=coords1.device, dtype=torch.float32)
         return self.corr_f32
 
     def lookup(self, corr_fn, coords1: Tensor):
-        """The correlation lookup as convc1's input (`raft.py:128`)."""
+        """The correlation lookup as convc1's input (`raft.py:128`): fp32 NHWC rows, split while convc1 stages them."""
         b, h, wd = self.shape
-        if hasattr(corr_fn, "lookup_nhwc"):  # CorrBlock: fp32 NHWC rows, split while convc1 stages them
-            corr_fn.lookup_nhwc(coords1, self.lookup_rows(coords1))
-            return _native.F32In(self.corr_f32, b, h, wd)
-        if self.corr is None:
-            self.corr = _native.s32_empty(b, h, wd, self.cgroups, coords1.device, zero=True)
-        corr_fn.lookup_s32(coords1, self.corr)
-        return _native.S32Slice(self.corr)
+        corr_fn.lookup_nhwc(coords1, self.lookup_rows(coords1))
+        return _native.F32In(self.corr_f32, b, h, wd)
 
     def update(self, corr_in, coords1: Tensor, need_mask: bool, mask_out: Optional[Tensor] = None) -> Optional[Tensor]:
-        """Everything of one update after the lookup; ``corr_in`` is convc1's input (F32In or S32Slice)."""
+        """Everything of one update after the lookup; ``corr_in`` is convc1's input (F32In)."""
         V, conv, w = _native.S32Slice, _native.conv_s32, self.w
         b, h, wd = self.shape
         # The motion encoder's two branches are independent (update.py:116-121): the flow branch (flow prep, convf1,

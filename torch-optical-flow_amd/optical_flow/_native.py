@@ -47,7 +47,6 @@ SYMBOLS = (
     "oflow_conv_s32",
     "oflow_pack_s32_f32",
     "oflow_flow_prep_s32",
-    "oflow_corr_lookup_tiled_s32",
     "oflow_conv_s32_ex",
     "oflow_stem_patches_s32",
     "oflow_norm_stats_finalize",
@@ -164,8 +163,6 @@ def load() -> ctypes.CDLL:
     lib.oflow_pack_s32_f32.argtypes = [P, L, I, I, I, I, I, I, P, L, P, L, P, I, P]
     lib.oflow_flow_prep_s32.restype = I
     lib.oflow_flow_prep_s32.argtypes = [P, I, I, I, P, P, L, P, L, P]
-    lib.oflow_corr_lookup_tiled_s32.restype = I
-    lib.oflow_corr_lookup_tiled_s32.argtypes = [PP, IP, IP, I, P, I, I, I, I, P, L, P]
     lib.oflow_corr_lookup_otf_f16.restype = I
     lib.oflow_corr_lookup_otf_f16.argtypes = [P, PP, IP, IP, I, P, I, I, I, I, I, P, P]
     lib.oflow_conv_s32_ex2.restype = I
@@ -690,15 +687,16 @@ class S32Slice:
 
 
 class F32In:
-    """Convolution input given as a dense fp32 NHWC tensor [B*H*W, C] (C % 32 == 0), split into hi + lo while the
-    kernel stages it (oflow_conv_s32_ex2, OFLOW_IN_F32; 1x1 convs): e.g. corr_lookup_tiled_nhwc's output."""
+    """Convolution input given as a dense fp32 NHWC tensor [B*H*W, C] (C % 4 == 0; the channels past C up to the next
+    multiple of 32 stage as zeros), split into hi + lo while the kernel stages it (oflow_conv_s32_ex2, OFLOW_IN_F32;
+    1x1 convs): the RAFT forward's lookup rows (corr_lookup_tiled_nhwc, C = L*(2r+1)^2 = 324)."""
 
     __slots__ = ("raw", "bhw")
     in_format = 2
 
     def __init__(self, raw: torch.Tensor, b: int, h: int, w: int):
-        if raw.dtype != torch.float32 or not raw.is_contiguous() or raw.shape[0] != b * h * w or raw.shape[1] % 32:
-            raise RuntimeError("F32In: raw must be contiguous fp32 [B*H*W, C], C % 32 == 0")
+        if raw.dtype != torch.float32 or not raw.is_contiguous() or raw.shape[0] != b * h * w or raw.shape[1] % 4:
+            raise RuntimeError("F32In: raw must be contiguous fp32 [B*H*W, C], C % 4 == 0")
         self.raw, self.bhw = raw, (int(b), int(h), int(w))
 
     @property
@@ -711,7 +709,7 @@ class F32In:
 
     @property
     def ng(self) -> int:
-        return int(self.raw.shape[1]) // 32
+        return (int(self.raw.shape[1]) + 31) // 32
 
     @property
     def device(self):
@@ -782,12 +780,8 @@ class ConvWeights:
 
     __slots__ = ("pack", "wscale", "bias", "n", "n_pad", "kh", "kw", "kg")
 
-    def __init__(self, weight: torch.Tensor, bias, n_pad: int, patches: bool = False, in_perm=None):
+    def __init__(self, weight: torch.Tensor, bias, n_pad: int, patches: bool = False):
         w = weight.detach().float()
-        if in_perm is not None:  # input channel i of the packing = weight channel in_perm[i] (-1: zero)
-            idx = in_perm.to(w.device)
-            wz = torch.cat([w, torch.zeros_like(w[:, :1])], dim=1)
-            w = wz[:, torch.where(idx < 0, torch.full_like(idx, w.shape[1]), idx)]
         if patches:  # kh x kw conv as a 1x1 over its patch matrix (flow_prep, stem_patches): channel k = t*C + c
             n, c, kh, kw = w.shape
             w = w.permute(0, 2, 3, 1).reshape(n, kh * kw * c, 1, 1)
@@ -945,33 +939,6 @@ def pack_s32(x: torch.Tensor, act: str, y0: S32Slice, y1=None, nhwc=None, dst_ch
         )
 
 
-def lookup_s32_stride(radius: int) -> int:
-    """Channels per pyramid level in the S32 lookup layout: (2r+1)^2 rounded up to 8."""
-    k = 2 * int(radius) + 1
-    return (k * k + 7) // 8 * 8
-
-
-def pack_lookup_s32(corr: torch.Tensor, num_levels: int, radius: int, out: torch.Tensor) -> torch.Tensor:
-    """A (B, L*(2r+1)^2, H, W) fp32 lookup output repacked into the S32 lookup layout (level l at l*LS)."""
-    kk = (2 * int(radius) + 1) ** 2
-    ls = lookup_s32_stride(radius)
-    dst = S32Slice(out)
-    for lvl in range(num_levels):
-        pack_s32(corr[:, lvl * kk : (lvl + 1) * kk], "none", dst, dst_channel=lvl * ls)
-    return out
-
-
-def lookup_s32_perm(num_levels: int, radius: int) -> torch.Tensor:
-    """Input-channel map of the S32 lookup layout: entry l*LS + k = l*(2r+1)^2 + k, -1 for the padding channels
-    (used to permute convc1's weights, ConvWeights(in_perm=...))."""
-    kk = (2 * int(radius) + 1) ** 2
-    ls = lookup_s32_stride(radius)
-    perm = torch.full((num_levels * ls,), -1, dtype=torch.long)
-    for lvl in range(num_levels):
-        perm[lvl * ls : lvl * ls + kk] = torch.arange(lvl * kk, (lvl + 1) * kk)
-    return perm
-
-
 def flow_prep(coords: torch.Tensor, patches: torch.Tensor, flow0=None, flow1=None) -> None:
     """coords1 (B, 2, H, W) -> convf1 patch matrix (S32, 4 groups) and the flow channels of the GRU inputs.
     flow0/flow1: (S32Slice, channel) pairs naming where the x flow channel lives (y follows it)."""
@@ -1024,9 +991,9 @@ def pyramid_grad_combine(grads) -> torch.Tensor:
 
 
 def corr_lookup_tiled_nhwc(pyr: TiledPyramid, coords: torch.Tensor, radius: int, out: torch.Tensor) -> torch.Tensor:
-    """``corr_lookup_tiled`` as fp32 NHWC rows into ``out`` [B*H*W, row] (row % 32 == 0): level l at channels
-    [l*LS, l*LS + (2r+1)^2) (LS = lookup_s32_stride(r)), every other channel written as 0 -- convc1's input
-    (F32In), the same permuted order as the S32 layout."""
+    """``corr_lookup_tiled`` as fp32 NHWC rows into ``out`` [B*H*W, row] (row >= L*(2r+1)^2; 16-B aligned), in the
+    reference's channel order (row q = ``corr[b, :, y, x]``); channels past L*(2r+1)^2 are left untouched. With
+    row = L*(2r+1)^2 this is exactly ``CorrBlock.__call__(coords).permute(0, 2, 3, 1)``: convc1's input (F32In)."""
     what = "corr_lookup"
     co = _gpu_f32(coords, "coords", what)
     b, _, h, w = co.shape
@@ -1042,30 +1009,6 @@ def corr_lookup_tiled_nhwc(pyr: TiledPyramid, coords: torch.Tensor, radius: int,
         _check(
             load().oflow_corr_lookup_tiled_nhwc_f32(ptrs, hs, ws, nl, co.data_ptr(), b, h, w, int(radius), out.data_ptr(),
                                                     int(out.shape[1]), _stream(co.device)),
-            what,
-        )
-    return out
-
-
-def corr_lookup_tiled_s32(pyr: TiledPyramid, coords: torch.Tensor, radius: int, out: torch.Tensor) -> torch.Tensor:
-    """``corr_lookup_tiled`` written as S32 into ``out`` (B, H, W, G, 2, 32): level l at channels [l*LS, l*LS + (2r+1)^2)
-    (LS = lookup_s32_stride(r)), zeros after each level; channels past L*LS are left untouched."""
-    what = "corr_lookup"
-    co = _gpu_f32(coords, "coords", what)
-    b, _, h, w = co.shape
-    nl = len(pyr.levels)
-    k = 2 * int(radius) + 1
-    if b * h * w != pyr.queries:
-        raise RuntimeError(f"{what}: coords {tuple(coords.shape)} do not match the pyramid's {pyr.queries} queries")
-    if out.dtype != torch.float16 or tuple(out.shape[:3]) != (b, h, w) or out.shape[3] * 32 < nl * lookup_s32_stride(radius):
-        raise RuntimeError(f"{what}: S32 output too small")
-    dst = S32Slice(out)
-    ptrs = (ctypes.c_void_p * nl)(*[t.data_ptr() for t in pyr.levels])
-    hs = (ctypes.c_int * nl)(*[d[0] for d in pyr.dims])
-    ws = (ctypes.c_int * nl)(*[d[1] for d in pyr.dims])
-    with torch.cuda.device(co.device), _Timed("corr_lookup", co.device):
-        _check(
-            load().oflow_corr_lookup_tiled_s32(ptrs, hs, ws, nl, co.data_ptr(), b, h, w, int(radius), dst.ptr, dst.ps, _stream(co.device)),
             what,
         )
     return out
