@@ -12,7 +12,9 @@ dataset or checkpoint is reachable offline.
 
 Printed (rank 0, one JSON line): pairs/s for the whole job, the lookup kernel's roofline (algorithmic bytes per
 launch / mean launch time from HIP events recorded on the launch stream inside the timed region), the corr
-pyramid kernel's MFMA rate, and the oracle (PyTorch-CPU restatement) timed on this host's cores.
+pyramid kernel's MFMA rate, ``epe_vs_reference`` (the benchmarked model on the reference's own golden pair, run
+in this process before timing), and the oracle (PyTorch-CPU restatement) timed on this host's cores on the
+workload's per-GPU batch. ``--pairs-per-gpu 1 --iters 24`` is predict.py's batch-1 latency case.
 """
 from __future__ import annotations
 
@@ -69,32 +71,82 @@ def mean_ms(events) -> float:
     return statistics.fmean(a.elapsed_time(b) for a, b in events)
 
 
-def cpu_baseline(h: int, w: int, iters: int):
-    """The oracle RAFT (PyTorch-CPU fp32, this host's threads) on 1 pair: 1 warm-up + median of 3 (~10-20 s)."""
+def _cpu_model() -> str:
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def cpu_baseline(h: int, w: int, iters: int, pairs: int):
+    """The oracle RAFT (PyTorch-CPU fp32 restatement of the reference, validated against its goldens) on this host:
+    torch threads = the CPUs this process may run on (sched_getaffinity), capped by OMP_NUM_THREADS where the box
+    sets the process's CPU share; 1 warm-up pair, then ``pairs`` pairs as one batch (configs #1 and
+    #3 / one 8-pair shard of #4 -- the workload's own per-GPU batch)."""
     from model import synthetic
     from oracle import raft as oraft
 
-    threads = torch.get_num_threads()
-    model = oraft.RAFT().eval()
-    model.load_state_dict(synthetic.synthetic_state_dict(model.state_dict()))
-    img0, img1 = synthetic.synthetic_pair(1, h, w)
-    padder = oraft.InputPadder(img0.shape)
-    p0, p1 = padder.pad(img0, img1)
-    times = []
-    with torch.inference_mode():
-        for i in range(4):
+    affinity = len(os.sched_getaffinity(0))
+    cap = int(os.environ.get("OMP_NUM_THREADS", affinity) or affinity)
+    threads = max(1, min(affinity, cap))
+    prev = torch.get_num_threads()
+    torch.set_num_threads(threads)
+    try:
+        model = oraft.RAFT().eval()
+        model.load_state_dict(synthetic.synthetic_state_dict(model.state_dict()))
+        img0, img1 = synthetic.synthetic_pair(pairs, h, w)
+        padder = oraft.InputPadder(img0.shape)
+        p0, p1 = padder.pad(img0, img1)
+        with torch.inference_mode():
+            model(p0[:1], p1[:1], iters=iters, test_mode=True)  # warm-up
             t = time.perf_counter()
             model(p0, p1, iters=iters, test_mode=True)
-            if i:
-                times.append(time.perf_counter() - t)
-    sec = statistics.median(times)
+            sec = time.perf_counter() - t
+    finally:
+        torch.set_num_threads(prev)
     return {
-        "value": round(1.0 / sec, 4),
+        "value": round(pairs / sec, 4),
         "unit": "image-pairs/s",
         "cores": threads,
+        "affinity_cpus": affinity,
+        "cpu_model": _cpu_model(),
         "kind": "port",
-        "sample": f"oracle RAFT (PyTorch-CPU fp32 restatement of the reference), 1 pair {h}x{w} padded, "
-        f"{iters} iters, test_mode; median of 3 after 1 warm-up ({sec:.2f} s/pair); torch threads={threads}",
+        "sample": f"oracle RAFT (PyTorch-CPU fp32 restatement of the reference), {pairs} pair(s) {h}x{w} padded as one "
+        f"batch, {iters} iters, test_mode, after a 1-pair warm-up: {sec:.2f} s ({sec / pairs:.2f} s/pair); "
+        f"torch threads={threads} of {affinity} CPUs in the affinity mask",
+    }
+
+
+def golden_epe(model, dev, workload: str):
+    """The reference's own flow for a golden pair (tests/golden/raft_e2e.npz, produced by the reference on CPU) vs this
+    build's forward with the same weights, run through the benchmarked model before timing: EPE of the 1/8-res flow
+    and of the (strided) full-res flow."""
+    import numpy as np
+
+    from model import InputPadder, synthetic
+
+    tag = "kitti" if workload == "kitti" else "sintel"
+    g = np.load(os.path.join(REPO, "tests", "golden", "raft_e2e.npz"), allow_pickle=False)
+    b, h, w, iters, s, seed = (int(v) for v in g[f"{tag}_cfg"])
+    img0, img1 = synthetic.synthetic_pair(b, h, w, seed=seed)
+    padder = InputPadder(img0.shape, mode=str(g[f"{tag}_mode"]))
+    p0, p1 = (x.to(dev) for x in padder.pad(img0, img1))
+    with torch.inference_mode():
+        low, up = model(p0, p1, iters=iters, test_mode=True)
+    up = padder.unpad(up)[..., ::s, ::s]
+    el = torch.norm(low.float().cpu() - torch.from_numpy(g[f"{tag}_low"]), dim=1)
+    eu = torch.norm(up.float().cpu() - torch.from_numpy(g[f"{tag}_up"]), dim=1)
+    return {
+        "case": f"golden '{tag}': {b} pair(s) {h}x{w}, {iters} iters, reference PyTorch-CPU flow",
+        "low_mean": float(el.mean()),
+        "low_max": float(el.max()),
+        "up_mean": float(eu.mean()),
+        "up_max": float(eu.max()),
+        "unit": "px",
     }
 
 
@@ -105,6 +157,7 @@ def main() -> int:
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--workload", default="sintel", choices=sorted(WORKLOADS))
     ap.add_argument("--pairs-per-gpu", type=int, default=None)
+    ap.add_argument("--iters", type=int, default=None, help="GRU iterations (default: the workload's 12)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-events", action="store_true", help="do not record per-kernel HIP events")
     ap.add_argument("--conv-events", action="store_true", help="also time every update-block conv launch")
@@ -130,6 +183,7 @@ def main() -> int:
 
     ppg, h, w, iters, pmode, alt = WORKLOADS[args.workload]
     ppg = args.pairs_per_gpu or ppg
+    iters = args.iters or iters
     global_batch = ppg * world
 
     torch.backends.cudnn.benchmark = not args.no_conv_benchmark
@@ -160,6 +214,10 @@ def main() -> int:
         img0 = a0.to(dev).repeat(reps, 1, 1, 1)[:global_batch].contiguous()
         img1 = a1.to(dev).repeat(reps, 1, 1, 1)[:global_batch].contiguous()
     padder = InputPadder((h, w), mode=pmode or "sintel")
+    dims = _native.pyramid_dims((h + 7) // 8, (w + 7) // 8, 4)
+    epe = golden_epe(model, dev, args.workload) if args.workload != "corr" and rank == 0 else None
+    shard_shape = (global_batch, 3, h, w)
+    flow_shapes = ((2, dims[0][0], dims[0][1]), (2, h, w))
 
     def forward(s0, s1):
         p0, p1 = padder.pad(s0, s1)
@@ -170,7 +228,7 @@ def main() -> int:
         if args.workload == "corr":
             return corr_step()
         if world > 1:
-            return infer_sharded(forward, img0, img1, dev)
+            return infer_sharded(forward, img0, img1, dev, shape=shard_shape, flow_shapes=flow_shapes)
         return forward(img0, img1)
 
     with torch.inference_mode():
@@ -199,7 +257,6 @@ def main() -> int:
     if rank == 0 and args.workload != "corr":
         assert out[1] is not None and out[1].shape == (global_batch, 2, h, w)
         assert torch.isfinite(out[1]).all()
-    dims = _native.pyramid_dims((h + 7) // 8, (w + 7) // 8, 4)
     pairs = global_batch * args.steps
     line = {
         "metric": METRIC,
@@ -212,8 +269,9 @@ def main() -> int:
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": ("f16 features / f32 accumulate (corr); " if alt else "f32 corr; ")
-        + ("update convs f32 as split-f16 hi+lo operands (3 MFMA/product, f32 accumulate)" if args.update_impl == "split" else "f32"),
+        "dtype": ("fp16 features, fp32 accumulate (on-the-fly corr); " if alt else "fp32 corr (fp32 MFMA); ")
+        + ("convs split-fp16 (22-bit operands: fp16 hi + lo, 3 MFMA per product, fp32 accumulate)"
+           if args.update_impl == "split" else "update convs fp32 (MIOpen)"),
         "data": "synthetic (integer texture frames with a known (3, -1.5) px shift; hash-initialised weights)",
         "config": {
             "workload": (f"corr-build+{iters}-lookups-fmaps-{ppg}x256x128x128" if args.workload == "corr"
@@ -279,8 +337,10 @@ def main() -> int:
                     "bytes_per_launch": nbytes,
                 }
             }
+    if epe is not None:
+        line["epe_vs_reference"] = {k: (round(v, 8) if isinstance(v, float) else v) for k, v in epe.items()}
     if rank == 0 and world == 1 and not args.no_cpu_baseline and args.workload in ("sintel", "kitti"):
-        line["cpu_baseline"] = cpu_baseline(h, w, iters)
+        line["cpu_baseline"] = cpu_baseline(h, w, iters, ppg)
     if rank == 0:
         print(json.dumps(line), flush=True)
     if world > 1:

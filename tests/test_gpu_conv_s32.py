@@ -260,3 +260,31 @@ def test_stem_patches_match_unfold(b, c, h, w):
     ref = unf.permute(0, 2, 1, 3, 4).reshape(b, 49 * c, ho, wo)  # -> t*C + c
     assert torch.equal(got[:, : 49 * c], ref)
     assert bool((got[:, 49 * c :] == 0).all())
+
+
+def test_range_check_fires_on_fp16_overflow(monkeypatch):
+    """OFLOW_CHECK=1 (here: the module flag it sets): a convolution input outside the fp16 range of the split operands
+    raises -- an S32 input whose hi half overflowed to inf, an fp32 input staged by the kernel, a normalise-on-load
+    input -- while in-range inputs pass."""
+    monkeypatch.setattr(N, "CHECK_RANGE", True)
+    g = torch.Generator().manual_seed(5)
+    b, c, h, w = 1, 64, 8, 12
+    x = torch.randn(b, c, h, w, generator=g).to(DEV)
+    cw = N.ConvWeights((torch.randn(32, c, 1, 1, generator=g) * 0.1).to(DEV), None, 32)
+    out = torch.empty(b, 32, h, w, device=DEV)
+    N.conv_s32(N.S32Slice(N.s32_from_f32(x)), cw, 32, f32=out)  # in range: runs
+    big = x.clone()
+    big[0, 5, 3, 4] = 7.0e4
+    with pytest.raises(RuntimeError, match="fp16 range"):
+        N.conv_s32(N.S32Slice(N.s32_from_f32(big)), cw, 32, f32=out)
+    rows = big.permute(0, 2, 3, 1).reshape(b * h * w, c).contiguous()
+    with pytest.raises(RuntimeError, match="fp16 range"):
+        N.conv_s32(N.F32In(rows, b, h, w), cw, 32, f32=out)
+    cw3 = N.ConvWeights((torch.randn(32, c, 3, 3, generator=g) * 0.1).to(DEV), None, 32)
+    scale = torch.ones(b, c, device=DEV)
+    shift = torch.zeros(b, c, device=DEV)
+    shift[0, 9] = 1.0e5
+    with pytest.raises(RuntimeError, match="fp16 range"):
+        N.conv_s32(N.NhwcNormIn(rows.clamp(-10, 10), b, h, w, scale, shift), cw3, 32, f32=out)
+    monkeypatch.setattr(N, "CHECK_RANGE", False)
+    N.conv_s32(N.S32Slice(N.s32_from_f32(big)), cw, 32, f32=out)  # off: no check, no raise

@@ -1,6 +1,7 @@
 """Parity of the gfx950 HIP path (through the C ABI of liboflow_hip.so) against the oracle and the goldens the
 reference produced. Tolerances: corr pyramid fp32 |d| <= 1e-4 + 1e-5|ref|; lookup |d| <= 1e-4;
-warp (0..255 frames) |d| <= 2e-3 (the reference's own CPU linspace is vector-width dependent at the ulp level);
+warp / grid_sample: bit-exact (every mode and padding: the kernel evaluates ATen's CPU arithmetic, fused
+multiply-adds included -- tools/exp/gridsample_emul.py pins that model against torch);
 end-to-end mean EPE <= 1e-4 px... see the individual tests.
 """
 import math
@@ -18,6 +19,17 @@ from oracle import corr as ocorr
 from oracle import operator as oop
 
 pytestmark = pytest.mark.gpu
+# the warp / grid_sample goldens and the live oracle run ATen's AVX512 CPU kernels; another host vector ISA may
+# contract differently, so a live comparison on such a host allows ulp-level noise (1e-5 of the value range)
+_EXACT_CPU = torch.backends.cpu.get_cpu_capability() == "AVX512"
+
+
+def _warp_close(got, ref, what):
+    err = (got - ref).abs().max().item() if got.numel() else 0.0
+    if _EXACT_CPU:
+        assert err == 0.0, (what, err)
+    else:
+        assert err <= 1e-5 * max(1.0, ref.abs().max().item()), (what, err)
 DEV = torch.device("cuda", 0)
 
 
@@ -165,6 +177,31 @@ def test_lookup_rejects_tiny_levels_q3():
         cb(coords_grid(1, 8, 12, device=DEV))
 
 
+def test_pyramid_full_size_fp64_spot_check():
+    """configs[1] shape (B=4, C=256, 128 x 128): levels 0-3 of the HIP pyramid (the tiled layout CorrBlock uses,
+    untiled) at 320 random queries against a float64 restatement of corr.py:38-54 (dot products / sqrt(C), floor 2x2
+    average pools), within SURVEY §8(c)'s fp32 tolerance |d| <= 1e-4 + 1e-5 |ref|."""
+    b, c, h, w = 4, 256, 128, 128
+    f1, f2 = synthetic.synthetic_fmaps(b, c, h, w, stream=17)
+    cb = CorrBlock(f1.to(DEV), f2.to(DEV))
+    got = [t.cpu().numpy() for t in cb.corr_pyramid]
+    a = f1.double().numpy().reshape(b, c, h * w)
+    m = f2.double().numpy().reshape(b, c, h * w)
+    qs = np.random.default_rng(1).integers(0, b * h * w, 320)
+    worst = 0.0
+    for q in qs:
+        bi, i = divmod(int(q), h * w)
+        lvl = (a[bi, :, i] @ m[bi] / math.sqrt(c)).reshape(h, w)
+        for l in range(4):
+            if l:
+                hh, ww = lvl.shape[0] // 2, lvl.shape[1] // 2
+                lvl = lvl[: 2 * hh, : 2 * ww].reshape(hh, 2, ww, 2).mean(axis=(1, 3))
+            d = np.abs(got[l][q, 0] - lvl)
+            assert (d <= 1e-4 + 1e-5 * np.abs(lvl)).all(), (q, l, float(d.max()))
+            worst = max(worst, float(d.max()))
+    print(f"configs[1] pyramid vs fp64: max |d| {worst:.2e} over 320 queries x 4 levels")
+
+
 def test_lookup_full_size_spot_check():
     """Config #2 shape (B=4, 128 x 128, C=256): spot-check 256 queries against the float64 oracle."""
     b, h, w = 4, 128, 128
@@ -203,12 +240,11 @@ def test_warp_matches_reference_goldens(golden):
         if key.startswith("warp_") and key != "warp_default":
             _, mode, pad, ac = key.split("_")
             out = optical_flow.warp(frame, flow, mode, pad, bool(int(ac))).cpu().numpy()
-            err = np.abs(out - g[key]).max()
-            assert err <= 2e-3, (key, err)
-    assert np.abs(optical_flow.warp(frame, flow).cpu().numpy() - g["warp_default"]).max() <= 2e-3
+            np.testing.assert_array_equal(out, g[key], err_msg=key)  # the reference's own outputs, bit for bit
+    np.testing.assert_array_equal(optical_flow.warp(frame, flow).cpu().numpy(), g["warp_default"])
     fp = torch.from_numpy(g["flow_px"]).to(DEV)
     out = optical_flow.integrate(fp, 0.5 * fp, -0.25 * fp).cpu().numpy()
-    assert np.abs(out - g["integrate_3"]).max() <= 2e-3
+    np.testing.assert_array_equal(out, g["integrate_3"])
 
 
 @pytest.mark.parametrize("mode", ["bilinear", "nearest", "bicubic"])
@@ -219,12 +255,7 @@ def test_warp_matches_oracle_sintel_frame(mode, pad, ac):
     flow = oop.normalize(torch.from_numpy(synthetic.hash_normal(6, (2, 2, 109, 256), 8.0)))
     ref = oop.warp(img0, flow, mode, pad, ac)
     got = optical_flow.warp(img0.to(DEV), flow.to(DEV), mode, pad, ac).cpu()
-    err = (got - ref).abs()
-    # nearest can flip a tap where the CPU and GPU grids differ by an ulp at a .5 boundary: allow a few
-    if mode == "nearest":
-        assert (err > 1e-3).float().mean().item() < 1e-3
-    else:
-        assert err.max().item() <= 2e-2 and err.mean().item() <= 1e-4
+    _warp_close(got, ref, (mode, pad, ac))
 
 
 @pytest.mark.parametrize("width", [331, 332])
@@ -241,9 +272,7 @@ def test_warp_bilinear_staged_and_direct_tiles(sigma, pad, width):
         flow = oop.normalize(px)
         ref = oop.warp(img0, flow, "bilinear", pad, ac)
         got = optical_flow.warp(img0.to(DEV), flow.to(DEV), "bilinear", pad, ac).cpu()
-        err = (got - ref).abs()
-        # as test_warp_matches_oracle_sintel_frame: ulp-level grid differences times the frame gradient
-        assert err.max().item() <= 2e-2 and err.mean().item() <= 1e-4, (sigma, pad, ac, err.max().item())
+        _warp_close(got, ref, (sigma, pad, ac))
 
 
 def test_grid_sample_and_bilinear_sampler_match_oracle():
@@ -261,7 +290,7 @@ def test_grid_sample_and_bilinear_sampler_match_oracle():
             for ac in (False, True):
                 r = F.grid_sample(x, grid, mode=mode, padding_mode=pad, align_corners=ac)
                 gg = _native.grid_sample(x.to(DEV), grid.to(DEV), mode, pad, ac).cpu()
-                assert (gg - r).abs().max().item() <= 1e-4, (mode, pad, ac)
+                _warp_close(gg, r, (mode, pad, ac))
 
 
 def test_ops_follow_the_current_stream():
@@ -317,16 +346,19 @@ def test_corrblock_pyramid_attribute_semantics():
     assert torch.equal(cb(coords)[:, 81:], 2 * before[:, 81:])
 
 
-def test_ops_refuse_autograd_inputs():
-    """The raw native ops have no autograd: an input that requires grad must raise, not silently drop the graph
-    (CorrBlock and optical_flow.warp wrap them in autograd Functions instead); under no_grad the same call runs."""
+def test_inference_layouts_refuse_autograd_inputs():
+    """The tiled / fp16 layouts have no autograd formula: an input that requires grad raises instead of silently
+    dropping the graph; the canonical ops (corr_pyramid / corr_lookup / grid_warp) differentiate instead."""
     f = torch.randn(1, 8, 16, 16, device=DEV, requires_grad=True)
     with pytest.raises(RuntimeError, match="requires grad"):
-        _native.corr_pyramid(f, f.detach(), 1)
+        _native.corr_pyramid_tiled(f, f.detach(), 1)
+    with pytest.raises(RuntimeError, match="requires grad"):
+        _native.otf_prepare(torch.randn(1, 32, 16, 16, device=DEV, requires_grad=True), torch.randn(1, 32, 16, 16, device=DEV), 1)
+    levels = _native.corr_pyramid(f, f.detach(), 1)
+    assert levels[0].requires_grad
     frame = torch.rand(1, 3, 8, 8, device=DEV, requires_grad=True)
     flow = torch.zeros(1, 2, 8, 8, device=DEV)
-    with pytest.raises(RuntimeError, match="requires grad"):
-        _native.grid_warp(frame, flow, "bilinear", "border", False)
+    assert _native.grid_warp(frame, flow, "bilinear", "border", False).requires_grad
     with torch.no_grad():
         assert optical_flow.warp(frame, flow).shape == frame.shape
 

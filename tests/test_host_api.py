@@ -102,3 +102,20 @@ def test_synthetic_generators_are_deterministic():
     # frame1(x) = frame0(x - (3, -1.5)): integer part of the shift checks exactly on the half-pixel lattice
     c0, c1 = synthetic.synthetic_pair(1, 40, 48, shift=(3.0, -2.0), seed=2)
     assert torch.equal(c1[..., 0:30, 10:40], c0[..., 2:32, 7:37])
+
+
+def test_load_state_dict_drops_packed_weight_caches():
+    """Parameters created under torch.inference_mode() have no version counter, so the split kernels' packed-weight
+    caches (keyed by storage) must be dropped when new weights are loaded in place."""
+    with torch.inference_mode():
+        model = RAFT()
+    mods = (model.fnet, model.cnet, model.update_block)
+    for m in mods:
+        m.__dict__["_split_weights"] = ("stale", {})
+    with torch.inference_mode():
+        model.load_state_dict(synthetic.synthetic_state_dict(model.state_dict()))
+    assert all("_split_weights" not in m.__dict__ for m in mods)
+    for m in mods:
+        m.__dict__["_split_weights"] = ("stale", {})
+    model.invalidate_weight_caches()
+    assert all("_split_weights" not in m.__dict__ for m in mods)

@@ -46,19 +46,67 @@ def _worker(rank, world, port, batch, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,batch", [(2, 8), (2, 5), (3, 7)])
-def test_scatter_gather_gloo(world, batch):
+def _run(target, world, *args):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, batch, q)) for r in range(world)]
+    procs = [ctx.Process(target=target, args=(r, world, port, *args, q)) for r in range(world)]
     for p in procs:
         p.start()
-    res = [q.get(timeout=120) for _ in range(world)]
+    res = [q.get(timeout=300) for _ in range(world)]
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
+    return res
+
+
+@pytest.mark.parametrize("world,batch", [(2, 8), (2, 5), (3, 7), (3, 2)])
+def test_scatter_gather_gloo(world, batch):
+    """Includes batch < world (rank 2 of (3, 2) holds no pair: it skips the forward and pads the gather)."""
+    res = _run(_worker, world, batch)
     assert all(all(r[1:]) for r in res), res
+
+
+def _oracle_worker(rank, world, port, batch, known_shape, q):
+    """The oracle RAFT (PyTorch-CPU restatement of the reference) sharded over gloo vs the same model unsharded."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.set_num_threads(2)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from model import synthetic
+        from oracle import raft as oraft
+
+        model = oraft.RAFT().eval()
+        model.load_state_dict(synthetic.synthetic_state_dict(model.state_dict()))
+        h, w = 128, 128  # level 3 = 2x2 (a 1-px level is NaN in the reference, Q3)
+        img0, img1 = synthetic.synthetic_pair(batch, h, w, seed=4)
+
+        def forward(a, b):
+            return model(a, b, iters=3, test_mode=True)
+
+        with torch.inference_mode():
+            shape = (batch, 3, h, w) if known_shape else None
+            flows = ((2, h // 8, w // 8), (2, h, w)) if known_shape else None
+            low, up = infer_sharded(forward, img0 if rank == 0 else None, img1 if rank == 0 else None,
+                                    torch.device("cpu"), shape=shape, flow_shapes=flows)
+            if rank == 0:
+                rl, ru = forward(img0, img1)
+                d = max(float((low - rl).abs().max()), float((up - ru).abs().max()))
+                q.put((rank, d, tuple(up.shape)))
+            else:
+                q.put((rank, 0.0 if low is None and up is None else 1.0, None))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,batch,known_shape", [(2, 3, True), (2, 2, False), (3, 2, True)])
+def test_oracle_raft_sharded_equals_unsharded(world, batch, known_shape):
+    """sharding pairs over ranks is exact -- each pair's flow from its rank equals the unsharded batch
+    run of the same model (per-pair math; the CPU convolutions are batch-size invariant to <= 1e-5 px)."""
+    res = sorted(_run(_oracle_worker, world, batch, known_shape))
+    assert res[0][2] == (batch, 2, 128, 128)
+    assert res[0][1] <= 1e-5, res
+    assert all(r[1] == 0.0 for r in res[1:]), res
 
 
 def test_shard_bounds_cover_batch():

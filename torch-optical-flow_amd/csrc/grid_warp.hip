@@ -1,11 +1,16 @@
 // Inverse warp by a flow field = F.grid_sample(frame, linspace-grid + flow) (gfx950).
 //
-// Replaces optical_flow/operator/operator.py:8-56 (warp -> warp_grid -> grid_sample). The base grid is
-// torch.linspace(-1, 1, n) evaluated in fp32 with ATen's two-sided formula (start + step*i below the halfway
-// index, end - step*(n-1-i) from it), flow is already in normalized units, and every grid_sample mode is
-// implemented with the CPU kernel's arithmetic forms (unnormalize (g+1)*((n-1)/2) or (g+1)*(n/2)-0.5,
-// e = 1-w weights, A = -0.75 cubic), so the result tracks the reference PyTorch-CPU path to ulp-level noise:
-//   mode: bilinear | nearest (round half to even) | bicubic;  padding: zeros | border | reflection.
+// Replaces optical_flow/operator/operator.py:8-56 (warp -> warp_grid -> grid_sample). Every arithmetic step is the
+// one ATen's CPU kernels perform on the reference path, so results are bit-identical to it (pinned by
+// tools/exp/gridsample_emul.py, a numpy model of those kernels that matches torch bit for bit). The CPU kernels are
+// compiled with FP contraction, which fixes where the fused multiply-adds sit:
+//   base grid  torch.linspace(-1, 1, n): fma(step, i, -1) below n/2, fma(-step, n-1-i, 1) from it (step = 2/(n-1))
+//   unnormalize  align_corners: (g+1) * ((n-1)/2);  else fma(g+1, n/2, -0.5)
+//   reflection   ATen's vectorised form: extra = fma(-trunc(|x-low|/2span), 2span, |x-low|), min(extra, 2span-extra)
+//   bilinear     fma(v_se, se, fma(v_sw, sw, fma(v_ne, ne, v_nw * nw)))  with nw = (1-ty)(1-tx) ...
+//   bicubic      A = -0.75 coefficients (inner polynomials fused), x-sums per padding instantiation (see row4), y-sum
+//                fma(c3, r3, fma(c2, r2, fma(c1, r1, c0 r0)))
+//   nearest      round half to even
 // Bilinear (the default mode): warp_bilinear_lds_kernel stages each 16 x 64 output tile's source box in LDS (below).
 // Other modes, and frames whose rows are not 16-B multiples: one thread per output pixel, flow read and output
 // writes coalesced along W; the gathered taps of neighbouring lanes are neighbours too for smooth flow.
@@ -29,23 +34,29 @@ struct WarpArgs {
 __device__ __forceinline__ float linspace_m1_p1(int i, int n) {
   if (n == 1) return -1.0f;
   const float step = 2.0f / static_cast<float>(n - 1);
-  return i < n / 2 ? -1.0f + step * static_cast<float>(i) : 1.0f - step * static_cast<float>(n - 1 - i);
+  return i < n / 2 ? fmaf(step, static_cast<float>(i), -1.0f) : fmaf(-step, static_cast<float>(n - 1 - i), 1.0f);
 }
 
 __device__ __forceinline__ float unnormalize(float g, int n, int ac) {
-  return ac ? (g + 1.0f) * (static_cast<float>(n - 1) / 2.0f) : (g + 1.0f) * (static_cast<float>(n) / 2.0f) - 0.5f;
+  return ac ? (g + 1.0f) * (static_cast<float>(n - 1) / 2.0f) : fmaf(g + 1.0f, static_cast<float>(n) / 2.0f, -0.5f);
 }
 
 __device__ __forceinline__ float clip(float x, int n) { return fminf(static_cast<float>(n - 1), fmaxf(x, 0.0f)); }
 
-__device__ __forceinline__ float reflect(float x, int twice_low, int twice_high) {
-  if (twice_low == twice_high) return 0.0f;
-  const float mn = static_cast<float>(twice_low) / 2.0f;
-  const float span = static_cast<float>(twice_high - twice_low) / 2.0f;
-  x = fabsf(x - mn);
-  const float extra = fmodf(x, span);
-  const int flips = static_cast<int>(floorf(x / span));
-  return (flips % 2 == 0) ? extra + mn : span - extra + mn;
+// ATen's vectorised reflect_coordinates: reflection about low and low + span, span = n-1 (align_corners, low = 0)
+// or n (low = -0.5)
+__device__ __forceinline__ float reflect(float x, int n, int ac) {
+  if (ac) {
+    if (n <= 1) return 0.0f;
+    const float ts = static_cast<float>(2 * (n - 1));
+    const float a = fabsf(x);
+    const float extra = fmaf(-truncf(a / ts), ts, a);
+    return fminf(extra, ts - extra);
+  }
+  const float ts = static_cast<float>(2 * n);
+  const float a = fabsf(x + 0.5f);
+  const float extra = fmaf(-truncf(a / ts), ts, a);
+  return fminf(extra, ts - extra) - 0.5f;
 }
 
 // padding applied to an unnormalized coordinate (ATen compute_coordinates)
@@ -53,7 +64,7 @@ __device__ __forceinline__ float pad_coord(float x, int n, int pad, int ac) {
   if (pad == OFLOW_PAD_BORDER) {
     x = clip(x, n);
   } else if (pad == OFLOW_PAD_REFLECTION) {
-    x = ac ? reflect(x, 0, 2 * (n - 1)) : reflect(x, -1, 2 * n - 1);
+    x = reflect(x, n, ac);
     x = clip(x, n);
   }
   return x;
@@ -73,11 +84,16 @@ __device__ __forceinline__ void cubic_coeffs(float t, float c[4]) {
   float x = t + 1.0f;
   c[0] = ((A * x - 5.0f * A) * x + 8.0f * A) * x - 4.0f * A;
   x = t;
-  c[1] = ((A + 2.0f) * x - (A + 3.0f)) * x * x + 1.0f;
+  c[1] = fmaf(fmaf(A + 2.0f, x, -(A + 3.0f)) * x, x, 1.0f);
   x = 1.0f - t;
-  c[2] = ((A + 2.0f) * x - (A + 3.0f)) * x * x + 1.0f;
+  c[2] = fmaf(fmaf(A + 2.0f, x, -(A + 3.0f)) * x, x, 1.0f);
   x = 2.0f - t;
   c[3] = ((A * x - 5.0f * A) * x + 8.0f * A) * x - 4.0f * A;
+}
+
+// ATen: (nw_val * nw) + (ne_val * ne) + (sw_val * sw) + (se_val * se), contracted
+__device__ __forceinline__ float bilerp(const float v[4], float nw, float ne, float sw, float se) {
+  return fmaf(v[3], se, fmaf(v[2], sw, fmaf(v[1], ne, v[0] * nw)));
 }
 
 template <int MODE, bool FLOW>
@@ -126,15 +142,16 @@ __global__ __launch_bounds__(256) void grid_warp_kernel(WarpArgs a) {
         float rows[4];
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-          float r = 0.0f;
+          float v[4];
 #pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            const float v = (xv[j] && yv[i]) ? s[yi[i] * a.W + xi[j]] : 0.0f;
-            r = j == 0 ? v * cx[0] : r + v * cx[j];
-          }
-          rows[i] = r;
+          for (int j = 0; j < 4; ++j) v[j] = (xv[j] && yv[i]) ? s[yi[i] * a.W + xi[j]] : 0.0f;
+          // the x-direction sum as ATen's instantiations evaluate it: reflection fuses the whole chain; zeros and
+          // border fuse only the first product
+          rows[i] = a.pad == OFLOW_PAD_REFLECTION
+                        ? fmaf(cx[3], v[3], fmaf(cx[2], v[2], fmaf(cx[1], v[1], cx[0] * v[0])))
+                        : (fmaf(cx[0], v[0], cx[1] * v[1]) + cx[2] * v[2]) + cx[3] * v[3];
         }
-        acc = rows[0] * cy[0] + rows[1] * cy[1] + rows[2] * cy[2] + rows[3] * cy[3];
+        acc = fmaf(cy[3], rows[3], fmaf(cy[2], rows[2], fmaf(cy[1], rows[1], cy[0] * rows[0])));
         dst[(size_t)c * HWo] = acc;
       }
     } else {
@@ -173,7 +190,7 @@ __global__ __launch_bounds__(256) void grid_warp_kernel(WarpArgs a) {
           }
 #pragma unroll
           for (int k = 0; k < 4; ++k)
-            if (c0 + k < a.C) dst[(size_t)(c0 + k) * HWo] = v[k][0] * nw + v[k][1] * ne + v[k][2] * sw + v[k][3] * se;
+            if (c0 + k < a.C) dst[(size_t)(c0 + k) * HWo] = bilerp(v[k], nw, ne, sw, se);
         }
       }
     }
@@ -308,7 +325,7 @@ __global__ __launch_bounds__(kWThreads) void warp_bilinear_lds_kernel(WarpArgs a
         }
 #pragma unroll
         for (int q = 0; q < 4; ++q)
-          if (c0 + q < a.C) d[(size_t)(c0 + q) * HWo] = v[q][0] * wnw[k] + v[q][1] * wne[k] + v[q][2] * wsw[k] + v[q][3] * wse[k];
+          if (c0 + q < a.C) d[(size_t)(c0 + q) * HWo] = bilerp(v[q], wnw[k], wne[k], wsw[k], wse[k]);
       }
     }
     return;
@@ -361,7 +378,8 @@ __global__ __launch_bounds__(kWThreads) void warp_bilinear_lds_kernel(WarpArgs a
         if (m & 4u) v2 = p[bw];
         if (m & 8u) v3 = p[bw + 1];
       }
-      dst[(size_t)c * HWo + yo * a.Wo + xo] = v0 * wnw[k] + v1 * wne[k] + v2 * wsw[k] + v3 * wse[k];
+      const float v[4] = {v0, v1, v2, v3};
+      dst[(size_t)c * HWo + yo * a.Wo + xo] = bilerp(v, wnw[k], wne[k], wsw[k], wse[k]);
     }
   }
 }

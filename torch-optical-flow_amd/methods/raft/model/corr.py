@@ -6,6 +6,10 @@
 * ``__call__`` — one launch of ``oflow_corr_lookup_tiled_f32`` for all levels: the (2r+1)^2 bilinear window per
   level, written straight into the (B, L*(2r+1)^2, H, W) fp32 NCHW output (`corr.py:56-77`, `utils.py:64-80`).
 
+Both are PyTorch operators (``torch.ops.oflow.corr_pyramid_tiled`` / ``corr_lookup_tiled``, csrc/torch_ops.cpp), so
+``torch.compile(fullgraph=True)`` traces ``__call__`` without graph breaks; under autograd the canonical
+``corr_pyramid`` / ``corr_lookup`` ops carry native backward formulas.
+
 Attributes match the reference: ``num_levels``, ``radius`` and ``corr_pyramid`` (list of (B*H*W, 1, H_l, W_l)
 fp32 tensors), the latter rebuilt bit-exactly from the tiles on first access (after which lookups use it, so
 in-place edits to it behave as in the reference). Divergence (documented): where a level is under 2 px in
@@ -13,63 +17,12 @@ H or W the reference returns NaN (it divides by W_l-1); this build raises ``Valu
 """
 from __future__ import annotations
 
-import math
 from typing import List, Optional
 
 import torch
 from torch import Tensor
 
 from optical_flow import _native
-
-
-class _CorrPyramidFn(torch.autograd.Function):
-    """Training path: the pyramid (canonical levels) with a native backward -- level gradients folded through the
-    average pools (oflow_corr_pyramid_grad_combine_f32), then grad_f1 = f2 . G^T / sqrt(C), grad_f2 = f1 . G / sqrt(C)
-    as batched GEMMs (rocBLAS via torch.bmm)."""
-
-    @staticmethod
-    def forward(ctx, fmap1: Tensor, fmap2: Tensor, num_levels: int):
-        ctx.save_for_backward(fmap1, fmap2)
-        return tuple(_native.corr_pyramid(fmap1, fmap2, num_levels))
-
-    @staticmethod
-    def backward(ctx, *grads):
-        f1, f2 = ctx.saved_tensors
-        b, c, h, w = f1.shape
-        n = h * w
-        levels = [
-            (g.contiguous().clone() if i == 0 else g.contiguous()) if g is not None else None for i, g in enumerate(grads)
-        ]
-        if levels[0] is None:
-            levels[0] = torch.zeros((b * n, 1, h, w), device=f1.device, dtype=torch.float32)
-        dims = _native.pyramid_dims(h, w, len(levels))
-        levels = [g if g is not None else torch.zeros((b * n, 1, *d), device=f1.device) for g, d in zip(levels, dims)]
-        g0 = _native.pyramid_grad_combine(levels).view(b, n, n)
-        s = 1.0 / math.sqrt(c)
-        f1m, f2m = f1.float().reshape(b, c, n), f2.float().reshape(b, c, n)
-        g1 = torch.bmm(f2m, g0.transpose(1, 2)).mul_(s).view(b, c, h, w)
-        g2 = torch.bmm(f1m, g0).mul_(s).view(b, c, h, w)
-        return g1.to(f1.dtype), g2.to(f2.dtype), None
-
-
-class _CorrLookupFn(torch.autograd.Function):
-    """Training path: the windowed lookup over canonical levels with the native transpose
-    (oflow_corr_lookup_backward_f32); coordinates get no gradient (the reference detaches them, raft.py:127)."""
-
-    @staticmethod
-    def forward(ctx, coords: Tensor, radius: int, *levels: Tensor):
-        ctx.save_for_backward(coords)
-        ctx.radius = radius
-        ctx.shapes = [tuple(t.shape) for t in levels]
-        ctx.device = coords.device
-        return _native.corr_lookup(list(levels), coords, radius)
-
-    @staticmethod
-    def backward(ctx, grad_out):
-        (coords,) = ctx.saved_tensors
-        grads = [torch.zeros(sh, device=ctx.device, dtype=torch.float32) for sh in ctx.shapes]
-        _native.corr_lookup_backward(grad_out.contiguous(), coords, ctx.radius, grads)
-        return (None, None, *grads)
 
 
 class CorrBlock:
@@ -80,8 +33,9 @@ class CorrBlock:
         self._tiled = None
         self._batch = fmap1.shape[0]
         if torch.is_grad_enabled() and (fmap1.requires_grad or fmap2.requires_grad):
-            # training (raft.py:149-175): canonical levels with native backward kernels
-            self._pyramid = list(_CorrPyramidFn.apply(fmap1, fmap2, num_levels))
+            # training (raft.py:149-175): canonical levels; oflow::corr_pyramid / corr_lookup carry the native
+            # backward (optical_flow/_ops.py)
+            self._pyramid = _native.corr_pyramid(fmap1, fmap2, num_levels)
             self._grad = True
             return
         self._grad = False
@@ -105,8 +59,6 @@ class CorrBlock:
     def __call__(self, coords: Tensor) -> Tensor:
         if self._tiled is not None:
             return _native.corr_lookup_tiled(self._tiled, coords, self.radius)
-        if torch.is_grad_enabled() and any(t.requires_grad for t in self._pyramid):
-            return _CorrLookupFn.apply(coords.detach(), self.radius, *self._pyramid)
         return _native.corr_lookup(self._pyramid, coords, self.radius)
 
     def lookup_nhwc(self, coords: Tensor, out: Tensor) -> Tensor:

@@ -5,8 +5,9 @@ in eval mode), so the only communication is at the edges of the batch (SURVEY.md
   * ``scatter_pairs``: rank ``src`` holds the global (B, 3, H, W) pair batch and scatters contiguous shards,
     one per rank (RCCL lowers scatter to per-peer sends: each peer receives over its own xGMI link);
   * ``gather_flows``:  shards' flows go back to rank ``dst``.
-There is no per-iteration exchange. Ragged batches (B % world_size != 0) are padded to equal chunks for the
-collective and trimmed on both sides. The same code runs on gloo with CPU tensors (tests).
+There is no per-iteration exchange, and with the global shape passed in (fixed per run) a step issues only the
+scatter and the two gathers: no metadata broadcast, no host sync. Ragged batches (B % world_size != 0) are padded
+to equal chunks for the collective and trimmed on both sides; a rank with no pair skips the forward. The same code runs on gloo with CPU tensors (tests).
 """
 from __future__ import annotations
 
@@ -29,12 +30,16 @@ def _world(group) -> Tuple[int, int]:
 
 
 def _meta(t: Optional[Tensor], src: int, group, device: torch.device) -> Sequence[int]:
+    """Broadcast ``t``'s shape from ``src`` (only when the caller does not pass it: one small collective + one host
+    sync). The rank count travels first, so zero-sized dimensions survive."""
     rank = dist.get_rank(group)
-    meta = torch.zeros(5, dtype=torch.int64, device=device)
+    meta = torch.zeros(9, dtype=torch.int64, device=device)
     if rank == src:
-        meta[: t.dim()] = torch.tensor(t.shape, dtype=torch.int64)
+        meta[0] = t.dim()
+        meta[1 : 1 + t.dim()] = torch.tensor(t.shape, dtype=torch.int64)
     dist.broadcast(meta, src=dist.get_global_rank(group, src) if group is not None else src, group=group)
-    return [int(v) for v in meta.tolist() if v != 0] if rank != src else list(t.shape)
+    v = meta.tolist()
+    return v[1 : 1 + v[0]]
 
 
 def scatter_pairs(
@@ -43,10 +48,13 @@ def scatter_pairs(
     device: torch.device,
     src: int = 0,
     group=None,
+    shape: Optional[Sequence[int]] = None,
 ) -> Tuple[Tensor, Tensor]:
-    """Scatter the pair batch held by rank ``src`` (other ranks pass ``None``); returns this rank's shard."""
+    """Scatter the pair batch held by rank ``src`` (other ranks pass ``None``); returns this rank's shard.
+    ``shape`` = the global (B, C, H, W) when every rank knows it (fixed per run: no metadata collective, no host
+    sync); otherwise it is broadcast from ``src``."""
     world, rank = _world(group)
-    shape = _meta(image0, src, group, device)
+    shape = list(shape) if shape is not None else _meta(image0, src, group, device)
     b, rest = shape[0], shape[1:]
     chunk = -(-b // world)
     start, stop = shard_bounds(b, world, rank)
@@ -95,12 +103,28 @@ def infer_sharded(
     device: torch.device,
     src: int = 0,
     group=None,
+    shape: Optional[Sequence[int]] = None,
+    flow_shapes: Optional[Tuple[Sequence[int], Sequence[int]]] = None,
 ) -> Tuple[Optional[Tensor], Optional[Tensor]]:
-    """scatter -> ``forward(shard0, shard1) -> (flow_low, flow_up)`` on every rank -> gather to ``src``."""
-    s0, s1 = scatter_pairs(image0, image1, device, src=src, group=group)
-    world, _ = _world(group)
-    global_batch = image0.shape[0] if dist.get_rank(group) == src else None
-    gb = torch.tensor([global_batch or 0], dtype=torch.int64, device=device)
-    dist.broadcast(gb, src=dist.get_global_rank(group, src) if group is not None else src, group=group)
-    low, up = forward(s0, s1)
-    return gather_flows(low, int(gb.item()), dst=src, group=group), gather_flows(up, int(gb.item()), dst=src, group=group)
+    """scatter -> ``forward(shard0, shard1) -> (flow_low, flow_up)`` on every rank -> gather to ``src``.
+
+    ``shape`` (global (B, C, H, W)) known on every rank makes a step collective-only: no metadata broadcast, no host
+    sync (bench.py passes it; shapes are fixed per run). A rank whose shard is empty (B < world size) does not run
+    ``forward``; it sends zero padding of ``flow_shapes`` = ((C, h, w) of flow_low, (C, H, W) of flow_up) -- without
+    them it runs ``forward`` on one zero pair to learn the shapes and discards the result."""
+    s0, s1 = scatter_pairs(image0, image1, device, src=src, group=group, shape=shape)
+    b = int(shape[0]) if shape is not None else None
+    if b is None:
+        gb = torch.tensor([image0.shape[0] if dist.get_rank(group) == src else 0], dtype=torch.int64, device=device)
+        dist.broadcast(gb, src=dist.get_global_rank(group, src) if group is not None else src, group=group)
+        b = int(gb.item())
+    if s0.shape[0] == 0:
+        if flow_shapes is None:
+            z = s0.new_zeros([1] + list(s0.shape[1:]))
+            lo, up = forward(z, z)
+            flow_shapes = (lo.shape[1:], up.shape[1:])
+        low = s0.new_zeros([0] + list(flow_shapes[0]))
+        up = s0.new_zeros([0] + list(flow_shapes[1]))
+    else:
+        low, up = forward(s0, s1)
+    return gather_flows(low, b, dst=src, group=group), gather_flows(up, b, dst=src, group=group)

@@ -51,6 +51,10 @@ def strip_module(state_dict: Dict[str, Tensor]) -> Dict[str, Tensor]:
     return {(k[7:] if k.startswith("module.") else k): v for k, v in state_dict.items()}
 
 
+def _drop_weight_cache(module: nn.Module, _incompatible) -> None:
+    module.__dict__.pop("_split_weights", None)
+
+
 class RAFT(nn.Module):
     def __init__(
         self,
@@ -98,6 +102,16 @@ class RAFT(nn.Module):
         # lookup per iteration on the main stream (both halves joined around it); "lane": each half looks up its own.
         self.pair_lanes = 2
         self.pair_lookup = "joined"
+        # the split paths cache packed fp16 hi/lo weights keyed by (storage, version); parameters created under
+        # torch.inference_mode() have no version counter, so loading new weights in place drops the caches
+        for m in (self.fnet, self.cnet, self.update_block):
+            m.register_load_state_dict_post_hook(_drop_weight_cache)
+
+    def invalidate_weight_caches(self) -> None:
+        """Drop the packed-weight caches of the split kernels (call after editing parameters in place under
+        torch.inference_mode(); load_state_dict does it by itself)."""
+        for m in (self.fnet, self.cnet, self.update_block):
+            _drop_weight_cache(m, None)
 
     # -- checkpoints -------------------------------------------------------------------------------------
     @classmethod
@@ -209,7 +223,14 @@ class RAFT(nn.Module):
         image1 = (2 * (image1 / 255.0) - 1.0).contiguous()
         hdim, cdim = self.hparams.hidden_dim, self.hparams.context_dim
 
-        split_enc = image0.is_cuda and not torch.is_grad_enabled() and self.encoder_impl == "split"
+        # the split encoders implement the inference forward: fnet in train mode with dropout > 0 applies Dropout2d in
+        # the reference (extractor.py BasicEncoder.forward), so it then runs as the module (cnet likewise: batch norm)
+        split_enc = (
+            image0.is_cuda
+            and not torch.is_grad_enabled()
+            and self.encoder_impl == "split"
+            and (not self.fnet.training or self.fnet.dropout is None)
+        )
         fnet = SplitEncoder(self.fnet) if split_enc else self.fnet
         cnet = SplitEncoder(self.cnet) if split_enc and not self.cnet.training else self.cnet
         block = AlternateCorrBlock if self.hparams.get("alternate_corr", False) else CorrBlock

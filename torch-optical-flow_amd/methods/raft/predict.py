@@ -116,7 +116,11 @@ def main(
     if eval_mode:
         model.eval()
 
-    pending = []
+    # writes overlap the next pairs' inference on one writer thread, at most WRITES_IN_FLIGHT behind: each slot owns
+    # its pinned host buffers (reused while the shape holds) and is waited on before reuse, which bounds host memory
+    # and re-raises a failed write at the next pair instead of after the whole folder
+    slots = [None] * WRITES_IN_FLIGHT
+    count = 0
     with torch.inference_mode(), ThreadPoolExecutor(max_workers=1) as writer:
         for i, (img0, img1) in enumerate(loader):
             img0 = img0.to(device, non_blocking=True)
@@ -127,22 +131,39 @@ def main(
             assert flow.shape[0] == 1
             flow = padder.unpad(flow)[0]
 
+            slot = slots[i % WRITES_IN_FLIGHT]
+            if slot is not None:
+                slot["future"].result()
+            else:
+                slot = slots[i % WRITES_IN_FLIGHT] = {"payload": None, "grid": None, "future": None}
             payload_dev = _native.flow_pack(flow.unsqueeze(0), 2, False)[0]
-            payload = torch.empty(payload_dev.shape, dtype=torch.float32, pin_memory=True)
-            payload.copy_(payload_dev, non_blocking=True)
+            payload = _pinned(slot, "payload", payload_dev)
             grid = png = None
             if visualize:
                 rgb = optical_flow.flow2rgb(flow)
-                grid_dev = image_grid([img0[0] / 255.0, img1[0] / 255.0, rgb])
-                grid = torch.empty(grid_dev.shape, dtype=torch.uint8, pin_memory=True)
-                grid.copy_(grid_dev, non_blocking=True)
+                grid = _pinned(slot, "grid", image_grid([img0[0] / 255.0, img1[0] / 255.0, rgb]))
                 png = destination / f"{i:06d}.png"
             done = torch.cuda.Event()
             done.record()
-            pending.append(writer.submit(_write_outputs, done, destination / f"{i:06d}.flo", payload, png, grid))
-        for p in pending:
-            p.result()
-    return len(pending)
+            slot["future"] = writer.submit(_write_outputs, done, destination / f"{i:06d}.flo", payload, png, grid)
+            count += 1
+        for slot in slots:
+            if slot is not None:
+                slot["future"].result()
+    return count
+
+
+WRITES_IN_FLIGHT = 3
+
+
+def _pinned(slot: dict, key: str, src: torch.Tensor) -> torch.Tensor:
+    """Copy ``src`` (device) into the slot's pinned host buffer ``key`` (allocated on first use or a shape change)
+    without blocking the host."""
+    buf = slot[key]
+    if buf is None or buf.shape != src.shape or buf.dtype != src.dtype:
+        buf = slot[key] = torch.empty(src.shape, dtype=src.dtype, pin_memory=True)
+    buf.copy_(src, non_blocking=True)
+    return buf
 
 
 def _cli(argv=None) -> int:

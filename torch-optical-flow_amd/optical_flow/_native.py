@@ -15,6 +15,8 @@ from typing import List, Sequence
 
 import torch
 
+from . import _ops
+
 _LIB_PATH = os.environ.get(
     "OFLOW_LIB", os.path.join(os.path.dirname(os.path.abspath(__file__)), "_lib", "liboflow_hip.so")
 )
@@ -184,8 +186,40 @@ def load() -> ctypes.CDLL:
     v = lib.oflow_abi_version()
     if v != ABI_VERSION:
         raise RuntimeError(f"liboflow_hip.so ABI version {v}, expected {ABI_VERSION}: rebuild the library")
+    _ops.load()  # torch.ops.oflow.* (liboflow_torch.so over this library)
     _lib = lib
     return lib
+
+
+def ops():
+    """The ``torch.ops.oflow`` namespace (loads both libraries on first use)."""
+    if _lib is None:
+        load()
+    return torch.ops.oflow
+
+
+def _run(what: str, device: torch.device, op, *args):
+    """``op(*args)``, bracketed by HIP events when the bench's recorder is on (kept out of traced graphs: with no
+    recorder this is a plain call, so torch.compile sees only the op)."""
+    if _recorder is None:
+        return op(*args)
+    with _Timed(what, device):
+        return op(*args)
+
+
+def _tensor(t, name: str, what: str) -> torch.Tensor:
+    if not isinstance(t, torch.Tensor):
+        raise TypeError(f"{what}: {name} must be a torch.Tensor")
+    return t
+
+
+def _no_grad_input(t: torch.Tensor, name: str, what: str) -> None:
+    """Ops without an autograd formula (the inference layouts) refuse inputs that would need one."""
+    if t.requires_grad and torch.is_grad_enabled():
+        raise RuntimeError(
+            f"{what}: {name} requires grad; this layout is inference-only (no backward): use CorrBlock's canonical "
+            "pyramid (corr_pyramid / corr_lookup have autograd), or run under torch.no_grad()"
+        )
 
 
 def _check(status: int, what: str) -> None:
@@ -227,36 +261,10 @@ def pyramid_dims(h: int, w: int, num_levels: int):
 
 
 def corr_pyramid(fmap1: torch.Tensor, fmap2: torch.Tensor, num_levels: int = 4) -> List[torch.Tensor]:
-    """Level l of the all-pairs correlation pyramid as (B*H*W, 1, H_l, W_l) fp32 views of one allocation."""
-    what = "corr_pyramid"
-    f1 = _gpu_f32(fmap1, "fmap1", what)
-    f2 = _gpu_f32(fmap2, "fmap2", what)
-    if f1.dim() != 4 or f1.shape != f2.shape:
-        raise RuntimeError(f"{what}: fmap1 {tuple(fmap1.shape)} and fmap2 {tuple(fmap2.shape)} must be equal (B, C, H, W)")
-    if f1.device != f2.device:
-        raise RuntimeError(f"{what}: fmap1 and fmap2 are on different devices")
-    b, c, h, w = f1.shape
-    dims = pyramid_dims(h, w, num_levels)
-    if b == 0:
-        return [torch.empty((0, 1, hl, wl), device=f1.device) for hl, wl in dims]
-    if any(hl < 1 or wl < 1 for hl, wl in dims):
-        raise RuntimeError(f"{what}: {num_levels} levels of 2x2 pooling need H, W >= {2 ** (num_levels - 1)}")
-    q = b * h * w
-    sizes = [q * hl * wl for hl, wl in dims]
-    buf = torch.empty(sum(sizes), device=f1.device, dtype=torch.float32)
-    levels, off = [], 0
-    for (hl, wl), n in zip(dims, sizes):
-        levels.append(buf[off : off + n].view(q, 1, hl, wl))
-        off += n
-    ptrs = (ctypes.c_void_p * num_levels)(*[lv.data_ptr() for lv in levels])
-    with torch.cuda.device(f1.device), _Timed("corr_pyramid", f1.device):
-        _check(
-            load().oflow_corr_pyramid_f32(
-                f1.data_ptr(), f2.data_ptr(), b, c, h, w, num_levels, ptrs, _stream(f1.device)
-            ),
-            what,
-        )
-    return levels
+    """Level l of the all-pairs correlation pyramid as (B*H*W, 1, H_l, W_l) fp32 (``torch.ops.oflow.corr_pyramid``;
+    differentiable in both feature maps)."""
+    f1, f2 = _tensor(fmap1, "fmap1", "corr_pyramid"), _tensor(fmap2, "fmap2", "corr_pyramid")
+    return list(_run("corr_pyramid", f1.device, ops().corr_pyramid, f1, f2, int(num_levels)))
 
 
 class TiledPyramid:
@@ -287,97 +295,25 @@ class TiledPyramid:
 def corr_pyramid_tiled(fmap1: torch.Tensor, fmap2: torch.Tensor, num_levels: int = 4) -> TiledPyramid:
     """The all-pairs correlation pyramid (same values as ``corr_pyramid``) in the tiled lookup layout."""
     what = "corr_pyramid"
-    f1 = _gpu_f32(fmap1, "fmap1", what)
-    f2 = _gpu_f32(fmap2, "fmap2", what)
-    if f1.dim() != 4 or f1.shape != f2.shape:
-        raise RuntimeError(f"{what}: fmap1 {tuple(fmap1.shape)} and fmap2 {tuple(fmap2.shape)} must be equal (B, C, H, W)")
-    if f1.device != f2.device:
-        raise RuntimeError(f"{what}: fmap1 and fmap2 are on different devices")
-    b, c, h, w = f1.shape
-    dims = pyramid_dims(h, w, num_levels)
-    if any(hl < 1 or wl < 1 for hl, wl in dims):
-        raise RuntimeError(f"{what}: {num_levels} levels of 2x2 pooling need H, W >= {2 ** (num_levels - 1)}")
-    q = b * h * w
-    per = [int(load().oflow_corr_tiled_level_floats(hl, wl)) for hl, wl in dims]
-    buf = torch.empty(max(1, q * sum(per)), device=f1.device, dtype=torch.float32)
-    levels, off = [], 0
-    for n in per:
-        levels.append(buf[off : off + q * n].view(q, n))
-        off += q * n
-    if q:
-        ptrs = (ctypes.c_void_p * num_levels)(*[lv.data_ptr() for lv in levels])
-        with torch.cuda.device(f1.device), _Timed("corr_pyramid", f1.device):
-            _check(
-                load().oflow_corr_pyramid_tiled_f32(f1.data_ptr(), f2.data_ptr(), b, c, h, w, num_levels, ptrs, _stream(f1.device)),
-                what,
-            )
-    return TiledPyramid(levels, dims, q)
+    f1, f2 = _tensor(fmap1, "fmap1", what), _tensor(fmap2, "fmap2", what)
+    _no_grad_input(f1, "fmap1", what)
+    _no_grad_input(f2, "fmap2", what)
+    levels = list(_run(what, f1.device, ops().corr_pyramid_tiled, f1, f2, int(num_levels)))
+    return TiledPyramid(levels, pyramid_dims(f1.shape[2], f1.shape[3], num_levels), int(levels[0].shape[0]))
 
 
 def corr_lookup_tiled(pyr: TiledPyramid, coords: torch.Tensor, radius: int) -> torch.Tensor:
-    """``corr_lookup`` on a ``TiledPyramid``: (B, L*(2r+1)^2, H, W) fp32."""
-    what = "corr_lookup"
-    co = _gpu_f32(coords, "coords", what)
-    if co.dim() != 4 or co.shape[1] != 2:
-        raise RuntimeError(f"{what}: coords must be (B, 2, H, W), got {tuple(coords.shape)}")
-    b, _, h, w = co.shape
-    nl = len(pyr.levels)
-    if b * h * w != pyr.queries:
-        raise RuntimeError(f"{what}: coords {tuple(coords.shape)} do not match the pyramid's {pyr.queries} queries")
-    if not 0 <= int(radius) <= MAX_RADIUS:
-        raise RuntimeError(f"{what}: radius {radius} outside [0, {MAX_RADIUS}]")
-    if pyr.levels[0].device != co.device:
-        raise RuntimeError(f"{what}: pyramid and coords are on different devices")
-    k = 2 * int(radius) + 1
-    out = torch.empty((b, nl * k * k, h, w), device=co.device, dtype=torch.float32)
-    if out.numel() == 0:
-        return out
-    ptrs = (ctypes.c_void_p * nl)(*[t.data_ptr() for t in pyr.levels])
-    hs = (ctypes.c_int * nl)(*[d[0] for d in pyr.dims])
-    ws = (ctypes.c_int * nl)(*[d[1] for d in pyr.dims])
-    with torch.cuda.device(co.device), _Timed("corr_lookup", co.device):
-        _check(
-            load().oflow_corr_lookup_tiled_f32(ptrs, hs, ws, nl, co.data_ptr(), b, h, w, int(radius), out.data_ptr(), _stream(co.device)),
-            what,
-        )
-    return out
+    """``corr_lookup`` on a ``TiledPyramid``: (B, L*(2r+1)^2, H, W) fp32 (``torch.ops.oflow.corr_lookup_tiled``)."""
+    co = _tensor(coords, "coords", "corr_lookup")
+    _no_grad_input(co, "coords", "corr_lookup")
+    return _run("corr_lookup", co.device, ops().corr_lookup_tiled, pyr.levels, co, int(radius))
 
 
 def corr_lookup(levels: Sequence[torch.Tensor], coords: torch.Tensor, radius: int) -> torch.Tensor:
-    """(B, L*(2r+1)^2, H, W) fp32 windowed lookup of ``levels`` at ``coords`` (B, 2, H, W)."""
-    what = "corr_lookup"
-    co = _gpu_f32(coords, "coords", what)
-    if co.dim() != 4 or co.shape[1] != 2:
-        raise RuntimeError(f"{what}: coords must be (B, 2, H, W), got {tuple(coords.shape)}")
-    b, _, h, w = co.shape
-    nl = len(levels)
-    if not 1 <= nl <= MAX_LEVELS:
-        raise RuntimeError(f"{what}: number of pyramid levels {nl} outside [1, {MAX_LEVELS}]")
-    if not 0 <= int(radius) <= MAX_RADIUS:
-        raise RuntimeError(f"{what}: radius {radius} outside [0, {MAX_RADIUS}]")
-    lv = []
-    for i, t in enumerate(levels):
-        t = _gpu_f32(t, f"corr_pyramid[{i}]", what)
-        if t.device != co.device:
-            raise RuntimeError(f"{what}: corr_pyramid[{i}] and coords are on different devices")
-        if t.dim() != 4 or t.shape[0] != b * h * w or t.shape[1] != 1:
-            raise RuntimeError(f"{what}: corr_pyramid[{i}] shape {tuple(t.shape)} != ({b * h * w}, 1, H_l, W_l)")
-        lv.append(t)
-    k = 2 * int(radius) + 1
-    out = torch.empty((b, nl * k * k, h, w), device=co.device, dtype=torch.float32)
-    if out.numel() == 0:
-        return out
-    ptrs = (ctypes.c_void_p * nl)(*[t.data_ptr() for t in lv])
-    hs = (ctypes.c_int * nl)(*[int(t.shape[2]) for t in lv])
-    ws = (ctypes.c_int * nl)(*[int(t.shape[3]) for t in lv])
-    with torch.cuda.device(co.device), _Timed("corr_lookup", co.device):
-        _check(
-            load().oflow_corr_lookup_f32(
-                ptrs, hs, ws, nl, co.data_ptr(), b, h, w, int(radius), out.data_ptr(), _stream(co.device)
-            ),
-            what,
-        )
-    return out
+    """(B, L*(2r+1)^2, H, W) fp32 windowed lookup of ``levels`` at ``coords`` (B, 2, H, W)
+    (``torch.ops.oflow.corr_lookup``; differentiable in the levels, coords get no gradient as in the reference)."""
+    co = _tensor(coords, "coords", "corr_lookup")
+    return _run("corr_lookup", co.device, ops().corr_lookup, list(levels), co.detach(), int(radius))
 
 
 def _modes(mode: str, padding_mode: str, what: str):
@@ -391,27 +327,12 @@ def _modes(mode: str, padding_mode: str, what: str):
 
 
 def grid_warp(frame: torch.Tensor, flow: torch.Tensor, mode: str, padding_mode: str, align_corners: bool) -> torch.Tensor:
-    """grid_sample(frame, linspace-grid + flow) with the grid never materialised."""
+    """grid_sample(frame, linspace-grid + flow) with the grid never materialised (``torch.ops.oflow.grid_warp``;
+    differentiable in frame and flow)."""
     what = "warp"
     m, p = _modes(mode, padding_mode, what)
-    fr = _gpu_f32(frame, "frame", what)
-    fl = _gpu_f32(flow, "flow", what)
-    if fr.dim() != 4 or fl.dim() != 4 or fl.shape[1] != 2 or fl.shape[0] != fr.shape[0] or fl.shape[2:] != fr.shape[2:]:
-        raise RuntimeError(f"{what}: frame {tuple(frame.shape)} must be (B, C, H, W) and flow {tuple(flow.shape)} (B, 2, H, W)")
-    if fr.device != fl.device:
-        raise RuntimeError(f"{what}: frame and flow are on different devices")
-    b, c, h, w = fr.shape
-    out = torch.empty_like(fr)
-    if out.numel() == 0:
-        return out
-    with torch.cuda.device(fr.device), _Timed("grid_warp", fr.device):
-        _check(
-            load().oflow_grid_warp_f32(
-                fr.data_ptr(), fl.data_ptr(), b, c, h, w, m, p, int(bool(align_corners)), out.data_ptr(), _stream(fr.device)
-            ),
-            what,
-        )
-    return out
+    fr, fl = _tensor(frame, "frame", what), _tensor(flow, "flow", what)
+    return _run("grid_warp", fr.device, ops().grid_warp, fr, fl, m, p, bool(align_corners))
 
 
 def convex_upsample(flow: torch.Tensor, mask: torch.Tensor) -> torch.Tensor:
@@ -493,98 +414,54 @@ def flow_pack(flow: torch.Tensor, channels: int, flip_rows: bool) -> torch.Tenso
 
 
 def grid_sample(inp: torch.Tensor, grid: torch.Tensor, mode: str, padding_mode: str, align_corners: bool) -> torch.Tensor:
-    """F.grid_sample for 4-D input (B, C, H, W) and grid (B, Ho, Wo, 2)."""
+    """F.grid_sample for 4-D input (B, C, H, W) and grid (B, Ho, Wo, 2) (``torch.ops.oflow.grid_sample``)."""
     what = "grid_sample"
     m, p = _modes(mode, padding_mode, what)
-    x = _gpu_f32(inp, "input", what)
-    g = _gpu_f32(grid, "grid", what)
-    if x.dim() != 4 or g.dim() != 4 or g.shape[-1] != 2 or g.shape[0] != x.shape[0]:
-        raise RuntimeError(f"{what}: input {tuple(inp.shape)} must be (B, C, H, W) and grid {tuple(grid.shape)} (B, Ho, Wo, 2)")
-    if x.device != g.device:
-        raise RuntimeError(f"{what}: input and grid are on different devices")
-    b, c, h, w = x.shape
-    ho, wo = g.shape[1], g.shape[2]
-    out = torch.empty((b, c, ho, wo), device=x.device, dtype=torch.float32)
-    if out.numel() == 0:
-        return out
-    with torch.cuda.device(x.device):
-        _check(
-            load().oflow_grid_sample_f32(
-                x.data_ptr(), g.data_ptr(), b, c, h, w, ho, wo, m, p, int(bool(align_corners)), out.data_ptr(), _stream(x.device)
-            ),
-            what,
-        )
-    return out
+    x, g = _tensor(inp, "input", what), _tensor(grid, "grid", what)
+    return _run("grid_sample", x.device, ops().grid_sample, x, g, m, p, bool(align_corners))
 
 
 def otf_prepare(fmap1: torch.Tensor, fmap2: torch.Tensor, num_levels: int = 4):
     """fmap1/sqrt(C) and the floor-pooled fmap2 pyramid as NHWC fp16 tensors (on-the-fly correlation inputs).
     Returns (f1h (B, H, W, C), [f2h_l (B, H_l, W_l, C)])."""
     what = "corr_otf_prepare"
-    f1 = _gpu_f32(fmap1, "fmap1", what)
-    f2 = _gpu_f32(fmap2, "fmap2", what)
-    if f1.dim() != 4 or f1.shape != f2.shape or f1.device != f2.device:
-        raise RuntimeError(f"{what}: fmap1 {tuple(fmap1.shape)} and fmap2 {tuple(fmap2.shape)} must be equal (B, C, H, W) on one device")
-    b, c, h, w = f1.shape
-    if c % 32 != 0:
-        raise RuntimeError(f"{what}: the fp16 MFMA path needs C % 32 == 0, got C={c}")
-    dims = pyramid_dims(h, w, num_levels)
-    if any(hl < 1 or wl < 1 for hl, wl in dims):
-        raise RuntimeError(f"{what}: {num_levels} levels of 2x2 pooling need H, W >= {2 ** (num_levels - 1)}")
-    f1h = torch.empty((b, h, w, c), device=f1.device, dtype=torch.float16)
-    f2h = [torch.empty((b, hl, wl, c), device=f1.device, dtype=torch.float16) for hl, wl in dims]
-    if b == 0:
-        return f1h, f2h
-    scratch = torch.empty(max(1, b * c * sum(hl * wl for hl, wl in dims[1:])), device=f1.device, dtype=torch.float32)
-    ptrs = (ctypes.c_void_p * num_levels)(*[t.data_ptr() for t in f2h])
-    with torch.cuda.device(f1.device), _Timed("corr_otf_prepare", f1.device):
-        _check(
-            load().oflow_corr_otf_prepare_f16(
-                f1.data_ptr(), f2.data_ptr(), b, c, h, w, num_levels, f1h.data_ptr(), ptrs, scratch.data_ptr(), _stream(f1.device)
-            ),
-            what,
-        )
-    return f1h, f2h
+    f1, f2 = _tensor(fmap1, "fmap1", what), _tensor(fmap2, "fmap2", what)
+    _no_grad_input(f1, "fmap1", what)
+    _no_grad_input(f2, "fmap2", what)
+    f1h, f2h = _run(what, f1.device, ops().corr_otf_prepare, f1, f2, int(num_levels))
+    return f1h, list(f2h)
 
 
 def corr_lookup_otf(f1h: torch.Tensor, f2h: Sequence[torch.Tensor], coords: torch.Tensor, radius: int) -> torch.Tensor:
     """(B, L*(2r+1)^2, H, W) fp32 lookup computed from the fp16 feature pyramid, no correlation volume."""
-    what = "corr_lookup_otf"
-    co = _gpu_f32(coords, "coords", what)
-    if co.dim() != 4 or co.shape[1] != 2:
-        raise RuntimeError(f"{what}: coords must be (B, 2, H, W), got {tuple(coords.shape)}")
-    b, _, h, w = co.shape
-    if f1h.dtype != torch.float16 or tuple(f1h.shape[:3]) != (b, h, w) or not f1h.is_contiguous():
-        raise RuntimeError(f"{what}: f1h {tuple(f1h.shape)} must be contiguous fp16 ({b}, {h}, {w}, C)")
-    c = int(f1h.shape[3])
-    nl = len(f2h)
-    if not 1 <= nl <= MAX_LEVELS:
-        raise RuntimeError(f"{what}: number of pyramid levels {nl} outside [1, {MAX_LEVELS}]")
-    if not 0 <= int(radius) <= 4:
-        raise RuntimeError(f"{what}: radius {radius} outside [0, 4]")
-    for i, t in enumerate(f2h):
-        if t.dtype != torch.float16 or t.dim() != 4 or t.shape[0] != b or t.shape[3] != c or not t.is_contiguous():
-            raise RuntimeError(f"{what}: fmap2 level {i} {tuple(t.shape)} must be contiguous fp16 ({b}, H_l, W_l, {c})")
-        if t.device != co.device:
-            raise RuntimeError(f"{what}: fmap2 level {i} and coords are on different devices")
-    k = 2 * int(radius) + 1
-    out = torch.empty((b, nl * k * k, h, w), device=co.device, dtype=torch.float32)
-    if out.numel() == 0:
-        return out
-    ptrs = (ctypes.c_void_p * nl)(*[t.data_ptr() for t in f2h])
-    hs = (ctypes.c_int * nl)(*[int(t.shape[1]) for t in f2h])
-    ws = (ctypes.c_int * nl)(*[int(t.shape[2]) for t in f2h])
-    with torch.cuda.device(co.device), _Timed("corr_lookup_otf", co.device):
-        _check(
-            load().oflow_corr_lookup_otf_f16(
-                f1h.data_ptr(), ptrs, hs, ws, nl, co.data_ptr(), b, c, h, w, int(radius), out.data_ptr(), _stream(co.device)
-            ),
-            what,
-        )
-    return out
+    co = _tensor(coords, "coords", "corr_lookup_otf")
+    _no_grad_input(co, "coords", "corr_lookup_otf")
+    return _run("corr_lookup_otf", co.device, ops().corr_lookup_otf, f1h, list(f2h), co, int(radius))
 
 
 ACT = {"none": 0, "relu": 1, "sigmoid": 2, "tanh": 3}
+
+# OFLOW_CHECK=1: before every split-fp16 convolution, a device-side max-abs reduction over its input (the values that
+# become fp16 hi + lo operands) raises if any |x| > 65504, where the hi half would overflow to inf. Debug mode: one
+# reduction and one host sync per convolution. Off by default (the checked RAFT activations stay below ~1e3).
+CHECK_RANGE = os.environ.get("OFLOW_CHECK", "0") not in ("", "0")
+F16_MAX = 65504.0
+
+
+def _range_check(x, what: str) -> None:
+    if isinstance(x, S32Slice):  # already split: an overflowed hi half is inf
+        v = x.t[:, :, :, x.g0 : x.g0 + x.ng, 0]
+    elif isinstance(x, NhwcNormIn):  # the kernel stages relu(raw * scale + shift)
+        b, h, w = x.bhw
+        c = x.raw.shape[1]
+        v = torch.relu(x.raw.view(b, h * w, c) * x.scale.view(b, 1, c) + x.shift.view(b, 1, c))
+    else:
+        v = x.raw
+    m = float(v.abs().amax().float()) if v.numel() else 0.0
+    if not m <= F16_MAX:
+        raise RuntimeError(
+            f"{what}: input max |x| = {m:g} is outside the fp16 range (65504) of the split-fp16 operands (OFLOW_CHECK)"
+        )
 
 
 def _chan_view(t: torch.Tensor, what: str):
@@ -820,6 +697,8 @@ def conv_s32(x: S32Slice, cw: ConvWeights, block_n: int, act: str = "none", out_
     fp32 destination. stats: instance-norm partials [B, conv_tiles(H, W), n_pad, 3]. res: S32Slice residual added
     after the activation, then res_act. epilogue 1/2: GRU gates / candidate with gru_h, gru_z ([P, CH] fp32)."""
     what = "conv_s32"
+    if CHECK_RANGE:
+        _range_check(x, f"{what} {cw.kh}x{cw.kw}")
     if x.ng != cw.kg:
         raise RuntimeError(f"{what}: input has {x.ng} groups, weights expect {cw.kg}")
     b, h, w = x.bhw
@@ -952,63 +831,24 @@ def flow_prep(coords: torch.Tensor, patches: torch.Tensor, flow0=None, flow1=Non
         _check(load().oflow_flow_prep_s32(co.data_ptr(), b, h, w, patches.data_ptr(), f0[0], f0[1], f1[0], f1[1], _stream(co.device)), "flow_prep")
 
 
-def corr_lookup_backward(grad_out: torch.Tensor, coords: torch.Tensor, radius: int, grads) -> None:
-    """Accumulate the lookup's input gradient into ``grads`` (canonical levels (B*H*W, 1, H_l, W_l) fp32, contiguous):
-    the transpose of corr_lookup for the same coords (which get no gradient, as in the reference)."""
-    what = "corr_lookup_backward"
-    go = _gpu_f32(grad_out, "grad_out", what)
-    co = _gpu_f32(coords, "coords", what)
-    b, _, h, w = co.shape
-    nl = len(grads)
-    for g in grads:
-        if g.dtype != torch.float32 or not g.is_contiguous() or g.shape[0] != b * h * w or g.device != co.device:
-            raise RuntimeError(f"{what}: gradient levels must be contiguous fp32 (B*H*W, 1, H_l, W_l)")
-    k = 2 * int(radius) + 1
-    if tuple(go.shape) != (b, nl * k * k, h, w):
-        raise RuntimeError(f"{what}: grad_out {tuple(go.shape)} does not match coords / levels")
-    ptrs = (ctypes.c_void_p * nl)(*[g.data_ptr() for g in grads])
-    hs = (ctypes.c_int * nl)(*[int(g.shape[-2]) for g in grads])
-    ws = (ctypes.c_int * nl)(*[int(g.shape[-1]) for g in grads])
-    with torch.cuda.device(co.device):
-        _check(load().oflow_corr_lookup_backward_f32(go.data_ptr(), co.data_ptr(), b, h, w, int(radius), ptrs, hs, ws, nl,
-                                                     _stream(co.device)), what)
+def corr_lookup_backward(grad_out: torch.Tensor, coords: torch.Tensor, radius: int, level0_hw, num_levels: int):
+    """The lookup's input gradient: the transpose of corr_lookup for the same coords (which get no gradient, as in
+    the reference), as new canonical levels (B*H*W, 1, H_l, W_l) fp32 for a level-0 size ``level0_hw``."""
+    h0, w0 = level0_hw
+    return list(ops().corr_lookup_backward(grad_out, coords, int(radius), int(h0), int(w0), int(num_levels)))
 
 
-def pyramid_grad_combine(grads) -> torch.Tensor:
-    """grads[0] += every coarser level's gradient pushed back through the floor 2x2 average pools; returns grads[0]."""
-    what = "corr_pyramid_backward"
-    nl = len(grads)
-    q = int(grads[0].shape[0])
-    for g in grads:
-        if g.dtype != torch.float32 or not g.is_contiguous() or g.shape[0] != q or g.device.type != "cuda":
-            raise RuntimeError(f"{what}: gradient levels must be contiguous fp32 CUDA (Q, 1, H_l, W_l)")
-    ptrs = (ctypes.c_void_p * nl)(*[g.data_ptr() for g in grads])
-    hs = (ctypes.c_int * nl)(*[int(g.shape[-2]) for g in grads])
-    ws = (ctypes.c_int * nl)(*[int(g.shape[-1]) for g in grads])
-    with torch.cuda.device(grads[0].device):
-        _check(load().oflow_corr_pyramid_grad_combine_f32(ptrs, hs, ws, nl, q, _stream(grads[0].device)), what)
-    return grads[0]
+def corr_pyramid_backward(level_grads, fmap1: torch.Tensor, fmap2: torch.Tensor):
+    """(grad_fmap1, grad_fmap2) from the pyramid level gradients: the floor-pool transpose (native kernel) and two
+    batched GEMMs."""
+    return tuple(ops().corr_pyramid_backward(list(level_grads), fmap1, fmap2))
 
 
 def corr_lookup_tiled_nhwc(pyr: TiledPyramid, coords: torch.Tensor, radius: int, out: torch.Tensor) -> torch.Tensor:
     """``corr_lookup_tiled`` as fp32 NHWC rows into ``out`` [B*H*W, row] (row >= L*(2r+1)^2; 16-B aligned), in the
     reference's channel order (row q = ``corr[b, :, y, x]``); channels past L*(2r+1)^2 are left untouched. With
     row = L*(2r+1)^2 this is exactly ``CorrBlock.__call__(coords).permute(0, 2, 3, 1)``: convc1's input (F32In)."""
-    what = "corr_lookup"
-    co = _gpu_f32(coords, "coords", what)
-    b, _, h, w = co.shape
-    nl = len(pyr.levels)
-    if b * h * w != pyr.queries:
-        raise RuntimeError(f"{what}: coords {tuple(coords.shape)} do not match the pyramid's {pyr.queries} queries")
-    if out.dtype != torch.float32 or not out.is_contiguous() or out.dim() != 2 or out.shape[0] != b * h * w:
-        raise RuntimeError(f"{what}: NHWC output must be contiguous fp32 [B*H*W, row]")
-    ptrs = (ctypes.c_void_p * nl)(*[t.data_ptr() for t in pyr.levels])
-    hs = (ctypes.c_int * nl)(*[d[0] for d in pyr.dims])
-    ws = (ctypes.c_int * nl)(*[d[1] for d in pyr.dims])
-    with torch.cuda.device(co.device), _Timed("corr_lookup", co.device):
-        _check(
-            load().oflow_corr_lookup_tiled_nhwc_f32(ptrs, hs, ws, nl, co.data_ptr(), b, h, w, int(radius), out.data_ptr(),
-                                                    int(out.shape[1]), _stream(co.device)),
-            what,
-        )
+    co = _tensor(coords, "coords", "corr_lookup")
+    _no_grad_input(co, "coords", "corr_lookup")
+    _run("corr_lookup", co.device, ops().corr_lookup_tiled_nhwc, pyr.levels, co, int(radius), out)
     return out

@@ -1,7 +1,9 @@
 """``optical_flow.operator`` drop-in (reference: optical_flow/operator/operator.py:8-165).
 
 ``warp`` runs on the gfx950 ``grid_warp`` kernel (the linspace base grid of ``warp_grid`` is fused into the
-kernel, never materialised). The flow rescaling helpers are single elementwise passes and stay plain PyTorch
+kernel, never materialised), registered as ``torch.ops.oflow.grid_warp`` with an autograd formula (frame and flow
+gradients through ATen's grid_sampler_2d_backward on the same grid, optical_flow/_ops.py), so it traces under
+torch.compile and differentiates in a photometric loss. The flow rescaling helpers are single elementwise passes and stay plain PyTorch
 tensor ops, exactly as the reference writes them. Signatures, defaults, the asserts and
 the quirks (Q8: ``warp`` is not the identity at zero flow with ``align_corners=False``; Q9: ``integrate`` passes
 un-normalised flow to ``warp``) are the reference's.
@@ -36,38 +38,7 @@ def warp(
     Returns:
         The warped image (B, C, H, W) fp32.
     """
-    if torch.is_grad_enabled() and (frame.requires_grad or flow.requires_grad):
-        return _WarpFn.apply(frame, flow, mode, padding_mode, align_corners)
     return _native.grid_warp(frame, flow, mode, padding_mode, align_corners)
-
-
-_INTERP = {"bilinear": 0, "nearest": 1, "bicubic": 2}
-_PAD = {"zeros": 0, "border": 1, "reflection": 2}
-
-
-class _WarpFn(torch.autograd.Function):
-    """``warp`` under autograd (e.g. a photometric loss in training): the forward on the HIP kernel, the backward
-    through ATen's grid_sampler_2d_backward on the reference's own grid (warp_grid, `operator.py:36-56`): the frame
-    gradient and the flow gradient (= the grid gradient: the base grid is constant)."""
-
-    @staticmethod
-    def forward(ctx, frame, flow, mode, padding_mode, align_corners):
-        ctx.save_for_backward(frame, flow)
-        ctx.args = (mode, padding_mode, bool(align_corners))
-        return _native.grid_warp(frame, flow, mode, padding_mode, align_corners)
-
-    @staticmethod
-    def backward(ctx, grad_out):
-        frame, flow = ctx.saved_tensors
-        mode, padding_mode, ac = ctx.args
-        grid = warp_grid(flow.float().permute(0, 2, 3, 1))
-        g_in, g_grid = torch.ops.aten.grid_sampler_2d_backward(
-            grad_out.contiguous(), frame.float(), grid, _INTERP[mode], _PAD[padding_mode], ac,
-            [ctx.needs_input_grad[0], ctx.needs_input_grad[1]],
-        )
-        g_frame = g_in.to(frame.dtype) if ctx.needs_input_grad[0] else None
-        g_flow = g_grid.permute(0, 3, 1, 2).to(flow.dtype) if ctx.needs_input_grad[1] else None
-        return g_frame, g_flow, None, None, None
 
 
 def warp_grid(flow: Tensor) -> Tensor:

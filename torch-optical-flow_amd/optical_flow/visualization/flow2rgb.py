@@ -55,7 +55,9 @@ def flow2rgb(
     elif max_norm is not None:
         # Python float + EPS is a double sum; the division by it runs in fp32
         denom = float(np.float32(max_norm + EPS))
-    rgb = _native.flow2rgb(flow, method, clip, denom, invert_y)
+    # a colour map has no useful gradient: detach, so a prediction that requires grad (the reference's own
+    # training_step logs flow2rgb(flow_predictions[-1]), raft.py:169-170) is visualised, not refused
+    rgb = _native.flow2rgb(flow.detach(), method, clip, denom, invert_y)
     if ndims == 3:
         rgb = rgb.view(*rgb.shape[-3:])
     return rgb
