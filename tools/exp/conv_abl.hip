@@ -1,3 +1,6 @@
+// EXPERIMENT (not product code): ablations of the product conv_s32 kernel (ABL bits; results wrong, timing only):
+// 1 no B writes in the loop, 2 no sub-step-1 operand reads (reuse sub-step 0's), 4 no sub-step-1 MFMAs, 8 no loads
+// in the loop, 16 no barriers in the loop.
 // Split-fp16 implicit-GEMM convolution for the RAFT update block (gfx950).
 //
 // Replaces the nn.Conv2d layers of methods/raft/model/update.py:40-161 (BasicMotionEncoder, SepConvGRU,
@@ -18,8 +21,8 @@
 // Workgroup tile: 4 output rows x 32 output columns (128 pixels) x BN output channels; 4 waves as WM x WN.
 // Loop: input groups (k32) outer, taps inner. Per group the (4 + KH - 1) x (32 + KW - 1) input halo is staged in
 // LDS once and read by every tap at a shifted offset; per (group, tap) a BN x 128-B weight slab is staged (double
-// buffered). Both are register-staged (B one step, the halo one group ahead). LDS lines are 16-B-slot swizzled
-// (slot ^= (row >> 1) & 7) so that the 32 rows of an MFMA operand read by ds_read_b128 are bank-conflict free.
+// buffered). Both are register-staged one step ahead. LDS rows are padded to 144 B so that the 32 rows of an MFMA operand
+// read by ds_read_b128 are bank-conflict free from any starting row, with affine (immediate-offset) addressing.
 // Epilogue: accumulators -> LDS tile [pixel][channel] fp32 -> per-channel scale, bias, activation and the fused
 // consumer (S32 stores with 16-B chunks, GRU gates, fp32 NCHW store/accumulate).
 #include "oflow_internal.h"
@@ -30,8 +33,6 @@ namespace {
 typedef _Float16 half8 __attribute__((ext_vector_type(8)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));  // native vector: stays in VGPRs (HIP uint4 is copied by memcpy)
-
-__device__ __forceinline__ int swz(int row) { return (row >> 1) & 7; }
 
 constexpr int kTY = 4, kTX = 32, kThreads = 256;  // default tile: kTY rows x kTX columns
 constexpr int kAinGroups = 4;                      // AIN inputs: up to 128 channels (the encoders' 64 / 96 / 128)
@@ -129,7 +130,7 @@ __device__ __forceinline__ void store_s32(uint8_t* y, long long ps, long long P,
 //   6. read sub-step 0's operands of step i+1                            -> in flight during 7
 //   7. MFMAs of sub-step 1
 // so every LDS read has a block of MFMAs to hide behind, and the one barrier per step sits between two MFMA blocks.
-template <int KH, int KW, int BN, int WM, int WN, int EPI, int TY = kTY, int AIN = kInS32>
+template <int KH, int KW, int BN, int WM, int WN, int EPI, int TY = kTY, int AIN = kInS32, int ABL = 0>
 __global__ __launch_bounds__(kThreads, 2) void conv_s32_kernel(ConvArgs a) {
   constexpr int T = KH * KW;
   constexpr int BM = TY * kTX;  // output pixels per workgroup (TY rows x 32 columns)
@@ -142,10 +143,10 @@ __global__ __launch_bounds__(kThreads, 2) void conv_s32_kernel(ConvArgs a) {
   static_assert(WM * WN == 4 && MT >= 1 && NT >= 1, "bad wave grid");
   // T == 1 (1x1 convs): the input tile changes every K-step, so A is staged like B (double buffered in LDS).
   constexpr bool ADB = (T == 1);
-  // 128-B LDS rows, 16-B slots XOR-swizzled (slot ^= (row >> 1) & 7): the 32 rows of an MFMA operand read by
-  // ds_read_b128 are bank-conflict free from any starting row (padded 144-B rows with affine addressing measured the
-  // same speed, tools/exp/conv_s32_dma.hip's history)
-  constexpr int RS = 128;
+  // LDS rows are 144 B (128 B of data + 16 B pad): rows r and r+1 start 36 banks apart, so the 16 rows one lane
+  // group of a ds_read_b128 reads (same 16-B chunk) fall on 16 distinct 4-bank groups (conflict-free), and every
+  // operand address is a per-lane base plus a compile-time offset (no per-read address arithmetic)
+  constexpr int RS = 144;
   constexpr int A_BYTES = NPIX * RS, B_BYTES = BN * RS;
   constexpr int MAIN_BYTES = (ADB ? 2 : 1) * A_BYTES + 2 * B_BYTES;
   constexpr int TS = BN + 4;              // epilogue tile row stride (floats)
@@ -231,10 +232,10 @@ __global__ __launch_bounds__(kThreads, 2) void conv_s32_kernel(ConvArgs a) {
           }                                                                                                          \
         }                                                                                                            \
         uint8_t* rw_ = sA + (BUF) * A_BYTES + p * RS + (c & 1) * 8;                                                  \
-        *reinterpret_cast<half4_*>(rw_ + (((c >> 1) ^ swz(p)) << 4)) = h4;                                           \
-        *reinterpret_cast<half4_*>(rw_ + (((4 + (c >> 1)) ^ swz(p)) << 4)) = l4;                                     \
+        *reinterpret_cast<half4_*>(rw_ + ((c >> 1) << 4)) = h4;                                           \
+        *reinterpret_cast<half4_*>(rw_ + ((4 + (c >> 1)) << 4)) = l4;                                     \
       } else {                                                                                                       \
-        *reinterpret_cast<u32x4*>(sA + (BUF) * A_BYTES + p * RS + ((c ^ swz(p)) << 4)) = RA[s_];                    \
+        *reinterpret_cast<u32x4*>(sA + (BUF) * A_BYTES + p * RS + (c << 4)) = RA[s_];                    \
       }                                                                                                              \
     }                                                                                                                \
   }
@@ -249,7 +250,7 @@ __global__ __launch_bounds__(kThreads, 2) void conv_s32_kernel(ConvArgs a) {
     const int item = tid + s_ * kThreads;                                                                            \
     const int n = item >> 3, c = item & 7;                                                                           \
     if (BITEMS % kThreads == 0 || item < BITEMS)                                                                     \
-      *reinterpret_cast<u32x4*>(sB + (BUF) * B_BYTES + n * RS + ((c ^ swz(n)) << 4)) = RB[s_];                      \
+      *reinterpret_cast<u32x4*>(sB + (BUF) * B_BYTES + n * RS + (c << 4)) = RB[s_];                      \
   }
   // operands of one 16-deep sub-step S_ of step I: A rows of this wave's pixel tiles at the step's tap offset, B rows
   // of its channel tiles; hi and lo halves
@@ -263,14 +264,14 @@ __global__ __launch_bounds__(kThreads, 2) void conv_s32_kernel(ConvArgs a) {
     _Pragma("unroll") for (int mt_ = 0; mt_ < MT; ++mt_) {                                                           \
       const int p_ = (wm * MT + mt_ + ky_) * HX + r + kx_;                                                           \
       const uint8_t* row_ = bufA_ + p_ * RS;                                                                         \
-      AH[mt_] = *reinterpret_cast<const half8*>(row_ + ((chi_ ^ swz(p_)) << 4));                                     \
-      AL[mt_] = *reinterpret_cast<const half8*>(row_ + ((clo_ ^ swz(p_)) << 4));                                     \
+      AH[mt_] = *reinterpret_cast<const half8*>(row_ + (chi_ << 4));                                     \
+      AL[mt_] = *reinterpret_cast<const half8*>(row_ + (clo_ << 4));                                     \
     }                                                                                                                \
     _Pragma("unroll") for (int nt_ = 0; nt_ < NT; ++nt_) {                                                           \
       const int n_ = wn * (BN / WN) + nt_ * 32 + r;                                                                  \
       const uint8_t* row_ = bufB_ + n_ * RS;                                                                         \
-      BH[nt_] = *reinterpret_cast<const half8*>(row_ + ((chi_ ^ swz(n_)) << 4));                                     \
-      BL[nt_] = *reinterpret_cast<const half8*>(row_ + ((clo_ ^ swz(n_)) << 4));                                     \
+      BH[nt_] = *reinterpret_cast<const half8*>(row_ + (chi_ << 4));                                     \
+      BL[nt_] = *reinterpret_cast<const half8*>(row_ + (clo_ << 4));                                     \
     }                                                                                                                \
   }
   // hi*lo + lo*hi + hi*hi per (pixel tile, channel tile): the lo*lo term is below fp32 rounding
@@ -323,15 +324,20 @@ __global__ __launch_bounds__(kThreads, 2) void conv_s32_kernel(ConvArgs a) {
     for (int t = 0; t < T; ++t) {
       const int i_ = g * T + t;
       // 1-2: step i+1's operands into the LDS buffers step i-1 used (free since step i-1's barrier); reload
-      OFLOW_WRITE_B(rb, (i_ + 1) & 1);
+      if constexpr (!(ABL & 1)) { OFLOW_WRITE_B(rb, (i_ + 1) & 1); }
       if constexpr (ADB) { OFLOW_WRITE_A(ra, (i_ + 1) & 1, i_ + 1 < S ? i_ + 1 : S - 1); }
-      {
+      if constexpr (!(ABL & 8)) {
         const int i2 = i_ + 2 < S ? i_ + 2 : S - 1;
         OFLOW_LOAD_B(rb, i2);
         if constexpr (ADB) { OFLOW_LOAD_A(ra, i2); }
       }
       // 3-4
-      OFLOW_READ_OPS(yah, yal, ybh, ybl, i_, 1);
+      if constexpr (!(ABL & 2)) {
+        OFLOW_READ_OPS(yah, yal, ybh, ybl, i_, 1);
+      } else {
+        for (int q = 0; q < MT; ++q) { yah[q] = xah[q]; yal[q] = xal[q]; }
+        for (int q = 0; q < NT; ++q) { ybh[q] = xbh[q]; ybl[q] = xbl[q]; }
+      }
       OFLOW_MFMAS(xah, xal, xbh, xbl);
       // 5: at the group's last tap the next group's halo replaces this one (loaded at the group's first tap)
       if constexpr (!ADB) {
@@ -339,13 +345,13 @@ __global__ __launch_bounds__(kThreads, 2) void conv_s32_kernel(ConvArgs a) {
           __syncthreads(); /* every wave is done reading A(g) */
           OFLOW_WRITE_A(ra, 0, g + 1 < a.kg ? g + 1 : g);
           const int g2 = g + 2 < a.kg ? g + 2 : a.kg - 1;
-          OFLOW_LOAD_A(ra, g2);
+          if constexpr (!(ABL & 8)) { OFLOW_LOAD_A(ra, g2); }
         }
       }
-      __syncthreads(); /* B(i+1) [A] visible; every read of step i done before step i+1 overwrites its buffers */
+      if constexpr (!(ABL & 16)) { __syncthreads(); }
       // 6-7
       OFLOW_READ_OPS(xah, xal, xbh, xbl, i_ + 1, 0);
-      OFLOW_MFMAS(yah, yal, ybh, ybl);
+      if constexpr (!(ABL & 4)) { OFLOW_MFMAS(yah, yal, ybh, ybl); }
     }
   }
 #undef OFLOW_MFMAS
@@ -532,70 +538,6 @@ __global__ __launch_bounds__(kThreads, 2) void conv_s32_kernel(ConvArgs a) {
   }
 }
 
-template <int KH, int KW, int BN, int WM, int WN, int EPI, int TY = kTY>
-int launch_conv(const ConvArgs& a0, hipStream_t s) {
-  ConvArgs a = a0;
-  a.tiles_y = (a.H + TY - 1) / TY;
-  dim3 grid(a.tiles_x * a.tiles_y * a.B, a.npad / BN);
-  if constexpr (KH == 3 && KW == 3 && EPI == 0) {  // the encoders' second block convs
-    if (a.ain == kInF32Norm) {
-      hipLaunchKernelGGL((conv_s32_kernel<KH, KW, BN, WM, WN, EPI, TY, kInF32Norm>), grid, dim3(kThreads), 0, s, a);
-      return launch_status();
-    }
-  }
-  if constexpr (KH == 1 && KW == 1 && EPI == 0 && BN == 128) {  // convc1 on the NHWC corr lookup
-    if (a.ain == kInF32) {
-      hipLaunchKernelGGL((conv_s32_kernel<KH, KW, BN, WM, WN, EPI, TY, kInF32>), grid, dim3(kThreads), 0, s, a);
-      return launch_status();
-    }
-  }
-  if (a.ain != kInS32) return OFLOW_E_MODE;
-  hipLaunchKernelGGL((conv_s32_kernel<KH, KW, BN, WM, WN, EPI, TY>), grid, dim3(kThreads), 0, s, a);
-  return launch_status();
-}
-
-template <int KH, int KW, int EPI>
-int launch_bn(const ConvArgs& a, int bn, hipStream_t s) {
-  switch (bn) {
-    case 128: return launch_conv<KH, KW, 128, 2, 2, EPI>(a, s);
-    case 96: return launch_conv<KH, KW, 96, 4, 1, EPI>(a, s);
-    case 64:
-      // 8-row tiles (each wave 64 px x 64 ch: 8 operand reads per 12 MFMAs instead of 6 per 6), except with
-      // instance-norm partials, whose layout is 4-row tiles
-      // (1x1 convs double-buffer the 8-row halo: 4-row tiles keep two workgroups per CU within the LDS)
-      if constexpr (KH * KW > 1)
-        if (a.stats == nullptr) return launch_conv<KH, KW, 64, 4, 1, EPI, 8>(a, s);
-      return launch_conv<KH, KW, 64, 2, 2, EPI>(a, s);
-    case 32: return launch_conv<KH, KW, 32, 4, 1, EPI>(a, s);
-    default: return OFLOW_E_SHAPE;
-  }
-}
-
-int dispatch_conv(const ConvArgs& a, int kh, int kw, int block_n, int epilogue, hipStream_t s) {
-  const int key = kh * 16 + kw;
-  switch (epilogue) {
-    case 0:
-      switch (key) {
-        case 0x11: return launch_bn<1, 1, 0>(a, block_n, s);
-        case 0x22: return launch_bn<2, 2, 0>(a, block_n, s);
-        case 0x33: return launch_bn<3, 3, 0>(a, block_n, s);
-        case 0x15: return launch_bn<1, 5, 0>(a, block_n, s);
-        case 0x51: return launch_bn<5, 1, 0>(a, block_n, s);
-        default: return OFLOW_E_SHAPE;
-      }
-    case 1:
-      if (block_n != 128) return OFLOW_E_SHAPE;
-      if (key == 0x15) return launch_conv<1, 5, 128, 2, 2, 1>(a, s);
-      if (key == 0x51) return launch_conv<5, 1, 128, 2, 2, 1>(a, s);
-      return OFLOW_E_SHAPE;
-    default:
-      if (block_n != 128) return OFLOW_E_SHAPE;
-      if (key == 0x15) return launch_conv<1, 5, 128, 2, 2, 2>(a, s);
-      if (key == 0x51) return launch_conv<5, 1, 128, 2, 2, 2>(a, s);
-      return OFLOW_E_SHAPE;
-  }
-}
-
 // argument checks + ConvArgs for oflow_conv_s32_ex
 int build_conv_args(ConvArgs& a, const void* d_x, long long x_pixel_stride, int in_groups, const void* d_wpack,
                     int n_pad, const float* d_wscale, const float* d_bias, int N, int B, int H, int W, int kh, int kw,
@@ -668,15 +610,37 @@ int build_conv_args(ConvArgs& a, const void* d_x, long long x_pixel_stride, int 
 
 using namespace oflow;
 
-extern "C" int oflow_conv_s32_ex2(const void* d_x, long long x_pixel_stride, int in_groups, const void* d_wpack,
-                                  int n_pad, const float* d_wscale, const float* d_bias, int N, int B, int H, int W, int kh,
-                                  int kw, int block_n, int epilogue, int activation, float out_scale, void* d_y0,
-                                  long long y0_pixel_stride, void* d_y1, long long y1_pixel_stride, float* d_f32,
-                                  long long f32_batch_stride, long long f32_channel_stride, int f32_accumulate,
-                                  float* d_gru_h, float* d_gru_z, int gru_channels, float* d_nhwc, int nhwc_pixel_stride,
-                                  float* d_stats, const void* d_res, long long res_pixel_stride, int res_activation,
-                                  int s2d, int in_format, const float* d_in_scale, const float* d_in_shift,
-                                  void* stream) {
+
+namespace {
+template <int ABL>
+int abl_launch(const ConvArgs& a0, int kh, int kw, int bn, int epi, hipStream_t s) {
+  ConvArgs a = a0;
+#define L(KH, KW, BN, WM, WN, EPI, TY)                                                                               \
+  {                                                                                                                  \
+    a.tiles_y = (a.H + TY - 1) / TY;                                                                                 \
+    dim3 grid(a.tiles_x * a.tiles_y * a.B, a.npad / BN);                                                             \
+    hipLaunchKernelGGL((conv_s32_kernel<KH, KW, BN, WM, WN, EPI, TY, kInS32, ABL>), grid, dim3(kThreads), 0, s, a); \
+    return launch_status();                                                                                          \
+  }
+  const int key = kh * 16 + kw;
+  if (epi == 1 && key == 0x15) L(1, 5, 128, 2, 2, 1, 4)
+  if (epi == 2 && key == 0x51) L(5, 1, 128, 2, 2, 2, 4)
+  if (epi == 0 && key == 0x33 && bn == 128) L(3, 3, 128, 2, 2, 0, 4)
+  if (epi == 0 && key == 0x33 && bn == 64) L(3, 3, 64, 4, 1, 0, 8)
+  if (epi == 0 && key == 0x11 && bn == 128) L(1, 1, 128, 2, 2, 0, 4)
+#undef L
+  return OFLOW_E_MODE;
+}
+}  // namespace
+
+extern "C" int exp_conv_abl(int abl, const void* d_x, long long x_pixel_stride, int in_groups, const void* d_wpack,
+                            int n_pad, const float* d_wscale, const float* d_bias, int N, int B, int H, int W, int kh,
+                            int kw, int block_n, int epilogue, int activation, float out_scale, void* d_y0,
+                            long long y0_pixel_stride, void* d_y1, long long y1_pixel_stride, float* d_f32,
+                            long long f32_batch_stride, long long f32_channel_stride, int f32_accumulate,
+                            float* d_gru_h, float* d_gru_z, int gru_channels, float* d_nhwc, int nhwc_pixel_stride,
+                            float* d_stats, const void* d_res, long long res_pixel_stride, int res_activation, int s2d,
+                            void* stream) {
   ConvArgs a;
   const int st = build_conv_args(a, d_x, x_pixel_stride, in_groups, d_wpack, n_pad, d_wscale, d_bias, N, B, H, W, kh, kw,
                                  block_n, epilogue, activation, out_scale, d_y0, y0_pixel_stride, d_y1, y1_pixel_stride,
@@ -684,49 +648,17 @@ extern "C" int oflow_conv_s32_ex2(const void* d_x, long long x_pixel_stride, int
                                  gru_channels, d_nhwc, nhwc_pixel_stride, d_stats, d_res, res_pixel_stride,
                                  res_activation, s2d);
   if (st != OFLOW_OK) return st;
-  if (in_format < kInS32 || in_format > kInF32) return OFLOW_E_MODE;
-  if (in_format != kInF32 && (x_pixel_stride & 127)) return OFLOW_E_ALIGN;  // S32 / dense fp32: whole 128-B groups
-  if (in_format == kInF32Norm && x_pixel_stride != (long long)in_groups * 128) return OFLOW_E_SHAPE;  // dense [P][kg*32]
-  if (in_format == kInF32) {  // rows of cin fp32 channels, (kg - 1) * 32 < cin <= kg * 32, cin % 4 == 0
-    const long long cin = x_pixel_stride / 4;
-    if ((x_pixel_stride & 15) || cin > (long long)in_groups * 32 || cin <= (long long)(in_groups - 1) * 32) return OFLOW_E_SHAPE;
-    a.cin = static_cast<int>(cin);
+  a.ain = kInS32;
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  switch (abl) {
+    case 0: return abl_launch<0>(a, kh, kw, block_n, epilogue, s);
+    case 1: return abl_launch<1>(a, kh, kw, block_n, epilogue, s);
+    case 2: return abl_launch<2>(a, kh, kw, block_n, epilogue, s);
+    case 4: return abl_launch<4>(a, kh, kw, block_n, epilogue, s);
+    case 8: return abl_launch<8>(a, kh, kw, block_n, epilogue, s);
+    case 16: return abl_launch<16>(a, kh, kw, block_n, epilogue, s);
+    case 25: return abl_launch<25>(a, kh, kw, block_n, epilogue, s);
+    case 27: return abl_launch<27>(a, kh, kw, block_n, epilogue, s);
+    default: return OFLOW_E_MODE;
   }
-  if (in_format == kInF32Norm) {  // normalised + ReLU'd on load
-    if (!d_in_scale || !d_in_shift) return OFLOW_E_NULL;
-    if (kh != 3 || kw != 3 || epilogue != 0 || in_groups > kAinGroups) return OFLOW_E_MODE;
-    a.ia = d_in_scale;
-    a.ib = d_in_shift;
-  } else if (in_format == kInF32) {
-    if (kh != 1 || kw != 1 || epilogue != 0 || block_n != 128) return OFLOW_E_MODE;
-  }
-  a.ain = in_format;
-  return dispatch_conv(a, kh, kw, block_n, epilogue, static_cast<hipStream_t>(stream));
-}
-
-extern "C" int oflow_conv_s32_ex(const void* d_x, long long x_pixel_stride, int in_groups, const void* d_wpack,
-                                 int n_pad, const float* d_wscale, const float* d_bias, int N, int B, int H, int W, int kh,
-                                 int kw, int block_n, int epilogue, int activation, float out_scale, void* d_y0,
-                                 long long y0_pixel_stride, void* d_y1, long long y1_pixel_stride, float* d_f32,
-                                 long long f32_batch_stride, long long f32_channel_stride, int f32_accumulate,
-                                 float* d_gru_h, float* d_gru_z, int gru_channels, float* d_nhwc, int nhwc_pixel_stride,
-                                 float* d_stats, const void* d_res, long long res_pixel_stride, int res_activation,
-                                 int s2d, void* stream) {
-  return oflow_conv_s32_ex2(d_x, x_pixel_stride, in_groups, d_wpack, n_pad, d_wscale, d_bias, N, B, H, W, kh, kw,
-                            block_n, epilogue, activation, out_scale, d_y0, y0_pixel_stride, d_y1, y1_pixel_stride,
-                            d_f32, f32_batch_stride, f32_channel_stride, f32_accumulate, d_gru_h, d_gru_z, gru_channels,
-                            d_nhwc, nhwc_pixel_stride, d_stats, d_res, res_pixel_stride, res_activation, s2d, kInS32,
-                            nullptr, nullptr, stream);
-}
-
-extern "C" int oflow_conv_s32(const void* d_x, long long x_pixel_stride, int in_groups, const void* d_wpack, int n_pad,
-                              const float* d_wscale, const float* d_bias, int N, int B, int H, int W, int kh, int kw,
-                              int block_n, int epilogue, int activation, float out_scale, void* d_y0,
-                              long long y0_pixel_stride, void* d_y1, long long y1_pixel_stride, float* d_f32,
-                              long long f32_batch_stride, long long f32_channel_stride, int f32_accumulate,
-                              float* d_gru_h, float* d_gru_z, int gru_channels, void* stream) {
-  return oflow_conv_s32_ex(d_x, x_pixel_stride, in_groups, d_wpack, n_pad, d_wscale, d_bias, N, B, H, W, kh, kw,
-                           block_n, epilogue, activation, out_scale, d_y0, y0_pixel_stride, d_y1, y1_pixel_stride,
-                           d_f32, f32_batch_stride, f32_channel_stride, f32_accumulate, d_gru_h, d_gru_z, gru_channels,
-                           nullptr, 0, nullptr, nullptr, 0, 0, 0, stream);
 }

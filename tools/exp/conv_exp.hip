@@ -1,5 +1,5 @@
 // EXPERIMENT (not product code): the product conv_s32 kernel with its VAR schedule hooks, for A/B timing in one process.
-#include "../../torch-optical-flow_amd/csrc/conv_s32.hip"
+#include "conv_s32_r01.hip"
 
 extern "C" int exp_conv_s32_var(int var, const void* d_x, long long x_pixel_stride, int in_groups, const void* d_wpack,
                                 int n_pad, const float* d_wscale, const float* d_bias, int N, int B, int H, int W, int kh,
@@ -21,6 +21,7 @@ extern "C" int exp_conv_s32_var(int var, const void* d_x, long long x_pixel_stri
     case 0: return oflow::dispatch_conv<0>(a, kh, kw, block_n, epilogue, s);
     case 1040: return oflow::dispatch_conv<1040>(a, kh, kw, block_n, epilogue, s);
     case 1072: return oflow::dispatch_conv<1072>(a, kh, kw, block_n, epilogue, s);
+    case 640: return oflow::dispatch_conv<640>(a, kh, kw, block_n, epilogue, s);
     default: return OFLOW_E_MODE;
   }
 }

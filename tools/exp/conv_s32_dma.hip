@@ -1,3 +1,8 @@
+// EXPERIMENT RECORD (not product code): the conv_s32 main loop with the weight slabs arriving by LDS-DMA
+// (buffer_load ... lds) into a 3-slot ring, waits and barriers in inline asm. Measured the same speed as the
+// register-staged product loop (profiles/r02/conv_ablation.json) although removing the slab's LDS stores altogether
+// saves 25 %: the LDS write traffic, not the store instructions, is what costs. It also failed the two-stream
+// pair-lanes equality test once (an unverified wait count), so it stays out of the product.
 // Split-fp16 implicit-GEMM convolution for the RAFT update block (gfx950).
 //
 // Replaces the nn.Conv2d layers of methods/raft/model/update.py:40-161 (BasicMotionEncoder, SepConvGRU,
@@ -17,9 +22,9 @@
 //
 // Workgroup tile: 4 output rows x 32 output columns (128 pixels) x BN output channels; 4 waves as WM x WN.
 // Loop: input groups (k32) outer, taps inner. Per group the (4 + KH - 1) x (32 + KW - 1) input halo is staged in
-// LDS once and read by every tap at a shifted offset; per (group, tap) a BN x 128-B weight slab is staged (double
-// buffered). Both are register-staged (B one step, the halo one group ahead). LDS lines are 16-B-slot swizzled
-// (slot ^= (row >> 1) & 7) so that the 32 rows of an MFMA operand read by ds_read_b128 are bank-conflict free.
+// LDS once and read by every tap at a shifted offset; per (group, tap) a BN x 128-B weight slab arrives by LDS-DMA
+// into a 3-slot ring (two steps ahead); the halo is register-staged one group ahead (main-loop comment below). LDS lines are 16-B-slot swizzled (slot ^= (row >> 1) & 7) so that the 32 rows of
+// an MFMA operand read by ds_read_b128 are bank-conflict free from any starting row.
 // Epilogue: accumulators -> LDS tile [pixel][channel] fp32 -> per-channel scale, bias, activation and the fused
 // consumer (S32 stores with 16-B chunks, GRU gates, fp32 NCHW store/accumulate).
 #include "oflow_internal.h"
@@ -121,33 +126,37 @@ __device__ __forceinline__ void store_s32(uint8_t* y, long long ps, long long P,
 // kInF32 = fp32 NHWC input split into hi + lo while staged (the NHWC corr lookup feeding convc1).
 //
 // Main loop (one K-step = one (input group, tap) pair = 32 input channels = two 16-deep MFMA sub-steps):
-//   1. write B(i+1) [1x1: and A(i+1)] from registers into its LDS buffer (loaded one step earlier)
-//   2. issue the global loads of B(i+2) [A(i+2)] (and, at a group's first tap, of the next group's halo)
+//   1. LDS-DMA of B(i+2) (global -> LDS directly, no registers) into the ring slot step i-1 used
+//   2. [1x1: A(i+1) written from registers, A(i+2) loaded]
 //   3. read sub-step 1's operands of step i from LDS                     -> in flight during 4
 //   4. 3 x MT x NT MFMAs of sub-step 0 (operands read during step i-1)
-//   5. barrier (at a group's last tap: first a barrier, then the next halo is written)
-//   6. read sub-step 0's operands of step i+1                            -> in flight during 7
-//   7. MFMAs of sub-step 1
-// so every LDS read has a block of MFMAs to hide behind, and the one barrier per step sits between two MFMA blocks.
+//   5. at a group's last tap: barrier, the next group's halo is written, the one after is loaded
+//   6. wait for this wave's B(i+1) DMA, barrier
+//   7. read sub-step 0's operands of step i+1                            -> in flight during 8
+//   8. MFMAs of sub-step 1
+// so every LDS read has a block of MFMAs to hide behind, one barrier per step sits between two MFMA blocks, and the
+// weights never pass through registers (their LDS stores cost as much as half the MFMAs when register-staged).
 template <int KH, int KW, int BN, int WM, int WN, int EPI, int TY = kTY, int AIN = kInS32>
 __global__ __launch_bounds__(kThreads, 2) void conv_s32_kernel(ConvArgs a) {
+#if defined(__HIP_DEVICE_COMPILE__)  // the host pass only needs the signature (the LDS-DMA builtins are device-only)
   constexpr int T = KH * KW;
   constexpr int BM = TY * kTX;  // output pixels per workgroup (TY rows x 32 columns)
   constexpr int PH = KH / 2, PW = KW / 2;
   constexpr int HY = TY + KH - 1, HX = kTX + KW - 1, NPIX = HY * HX;
   constexpr int AITEMS = NPIX * 8, APER = (AITEMS + kThreads - 1) / kThreads;
-  constexpr int BITEMS = BN * 8, BPER = (BITEMS + kThreads - 1) / kThreads;
   constexpr int MT = TY / WM;            // 32-pixel row tiles per wave
   constexpr int NT = BN / WN / 32;        // 32-channel column tiles per wave
   static_assert(WM * WN == 4 && MT >= 1 && NT >= 1, "bad wave grid");
+  constexpr int BDMA = BN / 32;           // 1-KB DMA instructions per wave per weight slab (BN x 128 B / 4 waves)
+  static_assert(BN % 32 == 0, "slab must split into whole 1-KB DMA blocks per wave");
   // T == 1 (1x1 convs): the input tile changes every K-step, so A is staged like B (double buffered in LDS).
   constexpr bool ADB = (T == 1);
   // 128-B LDS rows, 16-B slots XOR-swizzled (slot ^= (row >> 1) & 7): the 32 rows of an MFMA operand read by
-  // ds_read_b128 are bank-conflict free from any starting row (padded 144-B rows with affine addressing measured the
-  // same speed, tools/exp/conv_s32_dma.hip's history)
+  // ds_read_b128 are bank-conflict free from any starting row; the weight DMA applies the swizzle at the source
   constexpr int RS = 128;
   constexpr int A_BYTES = NPIX * RS, B_BYTES = BN * RS;
-  constexpr int MAIN_BYTES = (ADB ? 2 : 1) * A_BYTES + 2 * B_BYTES;
+  constexpr int NBUF = 3;                 // weight ring: step i reads slot i % 3 while i + 1 and i + 2 land
+  constexpr int MAIN_BYTES = (ADB ? 2 : 1) * A_BYTES + NBUF * B_BYTES;
   constexpr int TS = BN + 4;              // epilogue tile row stride (floats)
   constexpr int EPI_BYTES = BM * TS * 4;
   constexpr int LDS_BYTES = MAIN_BYTES > EPI_BYTES ? MAIN_BYTES : EPI_BYTES;
@@ -169,15 +178,13 @@ __global__ __launch_bounds__(kThreads, 2) void conv_s32_kernel(ConvArgs a) {
   const int n0 = blockIdx.y * BN;
   const long long pix0 = (long long)b * a.H * a.W;
 
-  // Register staging: one register set per operand; B(i+1) is written to LDS at step i's start and the set reloaded
-  // with B(i+2) right after. A (one group's halo) is loaded at the group's first tap and written at its last; for 1x1
-  // convs A follows B's scheme.
-  u32x4 ra[APER], rb[BPER];
+  // A (one group's halo) is register-staged: loaded one group ahead, written at the group's last tap; for 1x1 convs
+  // A follows the step (written at step i's start, reloaded right after).
+  u32x4 ra[APER];
   // Global loads are raw buffer loads: a per-lane 32-bit offset (fixed for the whole loop) plus the step's uniform
   // byte offset in an SGPR, so the loop spends no vector instructions on addresses. Every load is unconditional (no
   // exec branches), so the compiler counts vmcnt precisely: S32 halo pixels outside the image get an offset past the
   // buffer's end and load zeros; the fp32 input formats load a clamped in-image pixel that is zeroed when staged.
-  // B loads precede A loads in every step, so waiting for B never waits for the (HBM-latency) halo prefetch.
   const __amdgpu_buffer_rsrc_t rsA = __builtin_amdgcn_make_buffer_rsrc(
       const_cast<uint8_t*>(a.x + pix0 * a.xps), (short)0, (int)((long long)a.H * a.W * a.xps), 0x00020000);
   const __amdgpu_buffer_rsrc_t rsB =
@@ -197,9 +204,19 @@ __global__ __launch_bounds__(kThreads, 2) void conv_s32_kernel(ConvArgs a) {
     acol[s_] = c * 16;
     aok |= (ok ? 1u : 0u) << s_;
   }
-  int boff[BPER];
+  // weight DMA: wave w fills 1-KB blocks w*BDMA .. w*BDMA+BDMA-1 of the slab; lane k of block j lands in LDS slot
+  // q = 64 (w BDMA + j) + k = (row q / 8, physical slot q % 8), which holds logical 16-B chunk (q % 8) ^ swz(row)
+  int boff[BDMA];
 #pragma unroll
-  for (int s_ = 0; s_ < BPER; ++s_) boff[s_] = (n0 + (tid + s_ * kThreads) / 8) * 128 + ((tid + s_ * kThreads) & 7) * 16;
+  for (int j = 0; j < BDMA; ++j) {
+    const int q = (wave * BDMA + j) * 64 + lane, n = q >> 3;
+    boff[j] = (n0 + n) * 128 + (((q & 7) ^ swz(n)) << 4);
+  }
+#define OFLOW_DMA_B(BUF, STEP)                                                                                       \
+  _Pragma("unroll") for (int j_ = 0; j_ < BDMA; ++j_)                                                                \
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(                                                                        \
+        rsB, (__attribute__((address_space(3))) void*)(sB + (BUF) * B_BYTES + (wave * BDMA + j_) * 1024), 16,      \
+        boff[j_], (STEP) * a.npad * 128, 0, 0);
 #define OFLOW_LOAD_A(RA, G)                                                                                          \
   _Pragma("unroll") for (int s_ = 0; s_ < APER; ++s_) {                                                              \
     if constexpr (AIN == kInF32) /* rows of cin floats: channels past cin re-read the row's last 16 B (zeroed) */   \
@@ -238,27 +255,14 @@ __global__ __launch_bounds__(kThreads, 2) void conv_s32_kernel(ConvArgs a) {
       }                                                                                                              \
     }                                                                                                                \
   }
-#define OFLOW_LOAD_B(RB, STEP)                                                                                       \
-  _Pragma("unroll") for (int s_ = 0; s_ < BPER; ++s_) {                                                              \
-    const int item = tid + s_ * kThreads;                                                                            \
-    if (BITEMS % kThreads == 0 || item < BITEMS)                                                                     \
-      RB[s_] = __builtin_amdgcn_raw_buffer_load_b128(rsB, boff[s_], (STEP) * a.npad * 128, 0);                      \
-  }
-#define OFLOW_WRITE_B(RB, BUF)                                                                                       \
-  _Pragma("unroll") for (int s_ = 0; s_ < BPER; ++s_) {                                                              \
-    const int item = tid + s_ * kThreads;                                                                            \
-    const int n = item >> 3, c = item & 7;                                                                           \
-    if (BITEMS % kThreads == 0 || item < BITEMS)                                                                     \
-      *reinterpret_cast<u32x4*>(sB + (BUF) * B_BYTES + n * RS + ((c ^ swz(n)) << 4)) = RB[s_];                      \
-  }
   // operands of one 16-deep sub-step S_ of step I: A rows of this wave's pixel tiles at the step's tap offset, B rows
   // of its channel tiles; hi and lo halves
 #define OFLOW_READ_OPS(AH, AL, BH, BL, I, S_)                                                                        \
   {                                                                                                                  \
-    const int ii_ = (I);                                                                                              \
-    const int t_ = ii_ % T, ky_ = t_ / KW, kx_ = t_ - ky_ * KW;                                                       \
-    const uint8_t* bufA_ = sA + (ADB ? (ii_ & 1) * A_BYTES : 0);                                                      \
-    const uint8_t* bufB_ = sB + (ii_ & 1) * B_BYTES;                                                                  \
+    const int ii_ = (I);                                                                                             \
+    const int t_ = ii_ % T, ky_ = t_ / KW, kx_ = t_ - ky_ * KW;                                                      \
+    const uint8_t* bufA_ = sA + (ADB ? (ii_ & 1) * A_BYTES : 0);                                                     \
+    const uint8_t* bufB_ = sB + (ii_ % NBUF) * B_BYTES;                                                              \
     const int chi_ = 2 * (S_) + hh, clo_ = 4 + 2 * (S_) + hh;                                                        \
     _Pragma("unroll") for (int mt_ = 0; mt_ < MT; ++mt_) {                                                           \
       const int p_ = (wm * MT + mt_ + ky_) * HX + r + kx_;                                                           \
@@ -281,6 +285,10 @@ __global__ __launch_bounds__(kThreads, 2) void conv_s32_kernel(ConvArgs a) {
       acc[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(AL[mt], BH[nt], acc[mt][nt], 0, 0, 0);                    \
       acc[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(AH[mt], BH[nt], acc[mt][nt], 0, 0, 0);                    \
     }
+  // barriers are inline asm (with a memory clobber, so no LDS access moves across them): __syncthreads() would also
+  // wait for every outstanding DMA (vmcnt(0)), draining the weight ring's prefetch at each step
+#define OFLOW_BARRIER_LDS() asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory")
+#define OFLOW_BARRIER_VM(N) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"n"(N) : "memory")
 
   f32x16 acc[MT][NT];
 #pragma unroll
@@ -296,54 +304,62 @@ __global__ __launch_bounds__(kThreads, 2) void conv_s32_kernel(ConvArgs a) {
       sAff[e] = make_float2(a.ia[(long long)b * a.kg * 32 + e], a.ib[(long long)b * a.kg * 32 + e]);
     __syncthreads();
   }
-  // prologue: step 0 in LDS, step 1 in registers, sub-step 0 operands of step 0 read
-  OFLOW_LOAD_B(rb, 0);
+  // prologue: B(0), B(1) in flight to ring slots 0, 1; A(0) staged; the next A in registers; sub-step 0 operands read
+  OFLOW_DMA_B(0, 0);
+  OFLOW_DMA_B(1, S > 1 ? 1 : 0);
   OFLOW_LOAD_A(ra, 0);
   OFLOW_WRITE_A(ra, 0, 0);
-  OFLOW_WRITE_B(rb, 0);
-  {
-    const int i1 = S > 1 ? 1 : 0;
-    OFLOW_LOAD_B(rb, i1);
-    if constexpr (ADB) {
-      OFLOW_LOAD_A(ra, i1);
-    } else {
-      OFLOW_LOAD_A(ra, a.kg > 1 ? 1 : 0);
-    }
+  if constexpr (ADB) {
+    OFLOW_LOAD_A(ra, S > 1 ? 1 : 0);
+  } else {
+    OFLOW_LOAD_A(ra, a.kg > 1 ? 1 : 0);
   }
-  __syncthreads();
+  // B(0) landed (B(1) and the A prefetch may still be in flight)
+  OFLOW_BARRIER_VM(BDMA + APER);
   half8 xah[MT], xal[MT], xbh[NT], xbl[NT];  // sub-step 0 operands
   half8 yah[MT], yal[MT], ybh[NT], ybl[NT];  // sub-step 1 operands
   OFLOW_READ_OPS(xah, xal, xbh, xbl, 0, 0);
 
   // The loop body is one input group with its T taps unrolled (static tap index), and nothing in it is conditional:
-  // past the last step it re-loads / re-writes the last step's data into buffers no longer read, so the compiler
-  // sees every load and counts vmcnt exactly (a halo prefetch from HBM is never waited for by a weight write).
+  // past the last step it re-loads / re-writes the last step's data into buffers no longer read, so every wait count
+  // is static (a halo prefetch from HBM is never waited for by a weight step).
   for (int g = 0; g < a.kg; ++g) {
 #pragma unroll
     for (int t = 0; t < T; ++t) {
       const int i_ = g * T + t;
-      // 1-2: step i+1's operands into the LDS buffers step i-1 used (free since step i-1's barrier); reload
-      OFLOW_WRITE_B(rb, (i_ + 1) & 1);
-      if constexpr (ADB) { OFLOW_WRITE_A(ra, (i_ + 1) & 1, i_ + 1 < S ? i_ + 1 : S - 1); }
-      {
-        const int i2 = i_ + 2 < S ? i_ + 2 : S - 1;
-        OFLOW_LOAD_B(rb, i2);
-        if constexpr (ADB) { OFLOW_LOAD_A(ra, i2); }
+      // 1: B(i+2) into the slot step i-1 read (every wave finished those reads before step i-1's barrier)
+      OFLOW_DMA_B((i_ + 2) % NBUF, i_ + 2 < S ? i_ + 2 : S - 1);
+      // 2
+      if constexpr (ADB) {
+        OFLOW_WRITE_A(ra, (i_ + 1) & 1, i_ + 1 < S ? i_ + 1 : S - 1);
+        OFLOW_LOAD_A(ra, i_ + 2 < S ? i_ + 2 : S - 1);
       }
       // 3-4
       OFLOW_READ_OPS(yah, yal, ybh, ybl, i_, 1);
       OFLOW_MFMAS(xah, xal, xbh, xbl);
-      // 5: at the group's last tap the next group's halo replaces this one (loaded at the group's first tap)
+      // 5: at the group's last tap the next group's halo replaces this one
       if constexpr (!ADB) {
         if (t == T - 1) {
-          __syncthreads(); /* every wave is done reading A(g) */
+          OFLOW_BARRIER_LDS(); /* every wave is done reading A(g) */
           OFLOW_WRITE_A(ra, 0, g + 1 < a.kg ? g + 1 : g);
-          const int g2 = g + 2 < a.kg ? g + 2 : a.kg - 1;
-          OFLOW_LOAD_A(ra, g2);
+          OFLOW_LOAD_A(ra, g + 2 < a.kg ? g + 2 : a.kg - 1);
         }
       }
-      __syncthreads(); /* B(i+1) [A] visible; every read of step i done before step i+1 overwrites its buffers */
-      // 6-7
+      // 6: this wave's B(i+1) landed, then everyone's did. Younger than B(i+1) (issued at step i-1) and allowed to stay
+      // in flight: B(i+2), the 1x1 A(i+2), and the halo prefetches issued at a group's last tap (by step i-1 when
+      // t == 0, by this step when t == T-1) -- the halo is only waited for when it is written, T steps later
+      if constexpr (ADB) {
+        OFLOW_BARRIER_VM(BDMA + APER);
+      } else if constexpr (T == 2) {
+        OFLOW_BARRIER_VM(BDMA + APER);
+      } else {
+        if (t == 0 || t == T - 1) {
+          OFLOW_BARRIER_VM(BDMA + APER);
+        } else {
+          OFLOW_BARRIER_VM(BDMA);
+        }
+      }
+      // 7-8
       OFLOW_READ_OPS(xah, xal, xbh, xbl, i_ + 1, 0);
       OFLOW_MFMAS(yah, yal, ybh, ybl);
     }
@@ -352,8 +368,11 @@ __global__ __launch_bounds__(kThreads, 2) void conv_s32_kernel(ConvArgs a) {
 #undef OFLOW_READ_OPS
 #undef OFLOW_LOAD_A
 #undef OFLOW_WRITE_A
-#undef OFLOW_LOAD_B
-#undef OFLOW_WRITE_B
+#undef OFLOW_DMA_B
+#undef OFLOW_BARRIER_LDS
+#undef OFLOW_BARRIER_VM
+  // every DMA (the loop's last ones re-load into unread slots) has landed before the epilogue tile reuses the LDS
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
 
   // ---- epilogue: accumulators -> LDS tile [pixel][channel] ----
   float* sT = reinterpret_cast<float*>(smem);
@@ -530,6 +549,7 @@ __global__ __launch_bounds__(kThreads, 2) void conv_s32_kernel(ConvArgs a) {
       store_s32(a.y0, a.y0ps, P, n, a.N, hn);
     }
   }
+#endif
 }
 
 template <int KH, int KW, int BN, int WM, int WN, int EPI, int TY = kTY>

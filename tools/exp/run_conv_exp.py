@@ -26,8 +26,10 @@ class Proxy:
     var = 0
 
     def __getattr__(self, k):
-        if k == "oflow_conv_s32_ex":
-            return lambda *a: exp.exp_conv_s32_var(Proxy.var, *a)
+        if k == "oflow_conv_s32_ex2":  # the product wrapper's entry: S32 inputs only here (last 3 args in_format..)
+            if Proxy.var < 0:  # VAR -1: the current product kernel
+                return real.oflow_conv_s32_ex2
+            return lambda *a: exp.exp_conv_s32_var(Proxy.var, *a[:-4], a[-1])
         return getattr(real, k)
 
 
@@ -47,7 +49,32 @@ def timed(fn, n):
     return a.elapsed_time(b) / n
 
 
+def batch_scan():
+    """zr 1x5 at several batch sizes (workgroup-count quantization vs 2 workgroups per CU x 256 CUs)."""
+    dev = torch.device("cuda", 0)
+    g = torch.Generator().manual_seed(0)
+    wt = (torch.randn(256, 384, 1, 5, generator=g) * 0.03).to(dev)
+    cw = N.ConvWeights(wt, torch.zeros(256, device=dev), 256)
+    out = {}
+    for b in (1, 2, 4, 6, 8, 9, 10, 12, 16):
+        h, w = 55, 128
+        x = N.s32_from_f32(torch.randn(b, 384, h, w, generator=g).to(dev))
+        P = b * h * w
+        kw_ = dict(epilogue=1, y0=N.S32Slice(N.s32_empty(b, h, w, 4, dev)), gru_h=torch.randn(P, 128, device=dev),
+                   gru_z=torch.rand(P, 128, device=dev))
+        Proxy.var = 0
+        t = statistics.median(timed(lambda: N.conv_s32(N.S32Slice(x), cw, 128, **kw_), 10) for _ in range(3))
+        wgs = 4 * 14 * b * 2
+        out[b] = {"us": round(t * 1e3, 1), "us_per_pair": round(t * 1e3 / b, 1), "workgroups": wgs,
+                  "generations": round(wgs / 512, 3)}
+        print("zr batch", b, out[b], flush=True)
+    return out
+
+
 def main():
+    if os.environ.get("BATCH_SCAN"):
+        print(json.dumps(batch_scan()))
+        return
     b, h, w = 8, 55, 128
     dev = torch.device("cuda", 0)
     P = b * h * w
