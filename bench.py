@@ -162,6 +162,8 @@ def main() -> int:
     ap.add_argument("--no-events", action="store_true", help="do not record per-kernel HIP events")
     ap.add_argument("--conv-events", action="store_true", help="also time every update-block conv launch")
     ap.add_argument("--update-impl", default="split", choices=["split", "fused", "module"])
+    ap.add_argument("--graph", action="store_true",
+                    help="replay each rank's forward from a HIP graph (model/graph.py: one launch per step)")
     ap.add_argument("--no-conv-benchmark", action="store_true",
                     help="disable torch.backends.cudnn.benchmark (MIOpen exhaustive find of the conv algorithms)")
     args = ap.parse_args()
@@ -224,18 +226,33 @@ def main() -> int:
         low, up = model(p0, p1, iters=iters, test_mode=True)
         return low, padder.unpad(up)
 
+    fwd = forward
+    if args.graph and args.workload != "corr":
+        from model.graph import GraphedRAFT
+
+        # capture this rank's shard shape (padded), then every step copies the shard in and replays
+        pp = padder.pad(*(torch.zeros((ppg, 3, h, w), device=dev),) * 2)
+        with torch.inference_mode():
+            graphed = GraphedRAFT(model, pp[0], pp[1], iters=iters)
+
+        def fwd(s0, s1):
+            p0, p1 = padder.pad(s0, s1)
+            low, up = graphed(p0, p1)
+            return low, padder.unpad(up)
+
     def step():
         if args.workload == "corr":
             return corr_step()
         if world > 1:
-            return infer_sharded(forward, img0, img1, dev, shape=shard_shape, flow_shapes=flow_shapes)
-        return forward(img0, img1)
+            return infer_sharded(fwd, img0, img1, dev, shape=shard_shape, flow_shapes=flow_shapes)
+        return fwd(img0, img1)
 
     with torch.inference_mode():
         for _ in range(args.warmup):
             step()
         torch.cuda.synchronize(dev)
-        rec = ({"*": True} if args.conv_events else {}) if not args.no_events else None
+        # graph replays launch no Python, so no per-kernel events (the roofline comes from an eager run)
+        rec = ({"*": True} if args.conv_events else {}) if not (args.no_events or args.graph) else None
         _native.set_event_recorder(rec)
         if world > 1:
             dist.barrier()
@@ -266,6 +283,7 @@ def main() -> int:
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": round(1000.0 * elapsed / args.steps, 3),
+        "ms_per_pair": round(1000.0 * elapsed / args.steps / ppg, 3),
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
@@ -283,6 +301,7 @@ def main() -> int:
             "parallelism": f"pairs sharded over {world} GPU(s)" + (", RCCL scatter/gather" if world > 1 else ""),
             "conv_benchmark": not args.no_conv_benchmark,
             "update_impl": args.update_impl,
+            "hip_graph": bool(args.graph),
         },
     }
     if rec and args.conv_events:
@@ -295,7 +314,7 @@ def main() -> int:
             "corr_lookup_otf": {"launch_ms": round(mean_ms(lk), 4), "launches": len(lk)},
             "corr_otf_prepare": {"launch_ms": round(mean_ms(pp), 4) if pp else None},
         }
-    elif rec:
+    elif rec and rec.get("corr_lookup"):
         lk = rec.get("corr_lookup", [])
         pk = rec.get("corr_pyramid", [])
         lk_ms = mean_ms(lk)

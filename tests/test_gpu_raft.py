@@ -259,3 +259,20 @@ def test_raft_training_gradients_match_oracle():
     for k in ("fnet.conv1.weight", "fnet.layer3.1.conv2.weight", "update_block.gru.convz1.weight", "cnet.conv2.weight"):
         rel = float((prod[k] - orac[k]).norm() / orac[k].norm())
         assert rel <= 1e-3, (k, rel)
+
+
+def test_graphed_forward_equals_eager():
+    """model/graph.py: the forward replayed from a HIP graph (batch 1, 24 iterations: predict.py's case) gives the
+    eager forward's flows bit for bit, also after new inputs are copied in."""
+    from model.graph import GraphedRAFT
+
+    model = _model(RAFT)
+    pairs = [synthetic.synthetic_pair(1, 128, 160, seed=s) for s in (21, 22)]
+    padder = InputPadder(pairs[0][0].shape)
+    p = [[x.to(DEV) for x in padder.pad(a, b)] for a, b in pairs]
+    with torch.inference_mode():
+        g = GraphedRAFT(model, p[0][0], p[0][1], iters=24)
+        for a, b in p:
+            lo_e, up_e = model(a, b, iters=24, test_mode=True)
+            lo_g, up_g = g(a, b)
+            assert torch.equal(lo_g, lo_e) and torch.equal(up_g, up_e)

@@ -16,7 +16,7 @@ import torch  # noqa: E402
 
 from optical_flow import _native as N  # noqa: E402
 
-exp = ctypes.CDLL(os.path.join(HERE, "libconv_exp.so"))
+exp = ctypes.CDLL(os.path.join(HERE, os.environ.get("EXP_LIB", "libconv_exp.so")))
 real = N.load()
 exp.exp_conv_s32_var.restype = ctypes.c_int
 exp.exp_conv_s32_var.argtypes = [ctypes.c_int] + list(real.oflow_conv_s32_ex.argtypes)

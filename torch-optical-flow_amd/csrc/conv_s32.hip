@@ -33,7 +33,7 @@ typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));  // native vecto
 
 __device__ __forceinline__ int swz(int row) { return (row >> 1) & 7; }
 
-constexpr int kTY = 4, kTX = 32, kThreads = 256;  // default tile: kTY rows x kTX columns
+constexpr int kTY = 4, kTX = 32;  // default tile: kTY rows x kTX columns
 constexpr int kAinGroups = 4;                      // AIN inputs: up to 128 channels (the encoders' 64 / 96 / 128)
 
 
@@ -89,9 +89,10 @@ __device__ __forceinline__ float act_fn(float v, int act) {
 __device__ __forceinline__ void split8(const float* v, half8& hi, half8& lo) {
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
-    const _Float16 a = static_cast<_Float16>(v[j]);
-    hi[j] = a;
-    lo[j] = static_cast<_Float16>(v[j] - static_cast<float>(a));
+    _Float16 h_, l_;
+    split_f16(v[j], h_, l_);
+    hi[j] = h_;
+    lo[j] = l_;
   }
 }
 
@@ -109,9 +110,10 @@ __device__ __forceinline__ void store_s32(uint8_t* y, long long ps, long long P,
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       if (n + j < N) {
-        const _Float16 a = static_cast<_Float16>(v[j]);
-        hp[j] = a;
-        lp[j] = static_cast<_Float16>(v[j] - static_cast<float>(a));
+        _Float16 h_, l_;
+        split_f16(v[j], h_, l_);
+        hp[j] = h_;
+        lp[j] = l_;
       }
     }
   }
@@ -130,16 +132,17 @@ __device__ __forceinline__ void store_s32(uint8_t* y, long long ps, long long P,
 //   7. MFMAs of sub-step 1
 // so every LDS read has a block of MFMAs to hide behind, and the one barrier per step sits between two MFMA blocks.
 template <int KH, int KW, int BN, int WM, int WN, int EPI, int TY = kTY, int AIN = kInS32>
-__global__ __launch_bounds__(kThreads, 2) void conv_s32_kernel(ConvArgs a) {
+__global__ __launch_bounds__(64 * WM * WN, WM * WN == 8 ? 1 : 2) void conv_s32_kernel(ConvArgs a) {
+  constexpr int NTH = 64 * WM * WN;  // 4 waves (two workgroups per CU) or 8 (one)
   constexpr int T = KH * KW;
   constexpr int BM = TY * kTX;  // output pixels per workgroup (TY rows x 32 columns)
   constexpr int PH = KH / 2, PW = KW / 2;
   constexpr int HY = TY + KH - 1, HX = kTX + KW - 1, NPIX = HY * HX;
-  constexpr int AITEMS = NPIX * 8, APER = (AITEMS + kThreads - 1) / kThreads;
-  constexpr int BITEMS = BN * 8, BPER = (BITEMS + kThreads - 1) / kThreads;
+  constexpr int AITEMS = NPIX * 8, APER = (AITEMS + NTH - 1) / NTH;
+  constexpr int BITEMS = BN * 8, BPER = (BITEMS + NTH - 1) / NTH;
   constexpr int MT = TY / WM;            // 32-pixel row tiles per wave
   constexpr int NT = BN / WN / 32;        // 32-channel column tiles per wave
-  static_assert(WM * WN == 4 && MT >= 1 && NT >= 1, "bad wave grid");
+  static_assert((WM * WN == 4 || WM * WN == 8) && MT >= 1 && NT >= 1, "bad wave grid");
   // T == 1 (1x1 convs): the input tile changes every K-step, so A is staged like B (double buffered in LDS).
   constexpr bool ADB = (T == 1);
   // 128-B LDS rows, 16-B slots XOR-swizzled (slot ^= (row >> 1) & 7): the 32 rows of an MFMA operand read by
@@ -175,8 +178,8 @@ __global__ __launch_bounds__(kThreads, 2) void conv_s32_kernel(ConvArgs a) {
   u32x4 ra[APER], rb[BPER];
   // Global loads are raw buffer loads: a per-lane 32-bit offset (fixed for the whole loop) plus the step's uniform
   // byte offset in an SGPR, so the loop spends no vector instructions on addresses. Every load is unconditional (no
-  // exec branches), so the compiler counts vmcnt precisely: S32 halo pixels outside the image get an offset past the
-  // buffer's end and load zeros; the fp32 input formats load a clamped in-image pixel that is zeroed when staged.
+  // exec branches), so the compiler counts vmcnt precisely: halo pixels outside the image load a clamped in-image
+  // pixel that is zeroed when staged (not the buffer's out-of-range zero fill: that gave nondeterministic halos).
   // B loads precede A loads in every step, so waiting for B never waits for the (HBM-latency) halo prefetch.
   const __amdgpu_buffer_rsrc_t rsA = __builtin_amdgcn_make_buffer_rsrc(
       const_cast<uint8_t*>(a.x + pix0 * a.xps), (short)0, (int)((long long)a.H * a.W * a.xps), 0x00020000);
@@ -187,19 +190,19 @@ __global__ __launch_bounds__(kThreads, 2) void conv_s32_kernel(ConvArgs a) {
   unsigned aok = 0u;
 #pragma unroll
   for (int s_ = 0; s_ < APER; ++s_) {
-    const int item = (AITEMS % kThreads == 0) ? tid + s_ * kThreads : min(tid + s_ * kThreads, AITEMS - 1);
+    const int item = (AITEMS % NTH == 0) ? tid + s_ * NTH : min(tid + s_ * NTH, AITEMS - 1);
     const int p = item >> 3, c = item & 7;
     const int gy = ty0 - PH + p / HX, gx = tx0 - PW + p % HX;
     const bool ok = static_cast<unsigned>(gy) < static_cast<unsigned>(a.H) && static_cast<unsigned>(gx) < static_cast<unsigned>(a.W);
     const int cy = min(max(gy, 0), a.H - 1), cx = min(max(gx, 0), a.W - 1);
     const int off = (cy * a.W + cx) * (int)a.xps + (AIN == kInF32 ? 0 : c * 16);
-    aoff[s_] = (AIN == kInS32 && !ok) ? (int)0x80000000 : off;
+    aoff[s_] = off;
     acol[s_] = c * 16;
     aok |= (ok ? 1u : 0u) << s_;
   }
   int boff[BPER];
 #pragma unroll
-  for (int s_ = 0; s_ < BPER; ++s_) boff[s_] = (n0 + (tid + s_ * kThreads) / 8) * 128 + ((tid + s_ * kThreads) & 7) * 16;
+  for (int s_ = 0; s_ < BPER; ++s_) boff[s_] = (n0 + (tid + s_ * NTH) / 8) * 128 + ((tid + s_ * NTH) & 7) * 16;
 #define OFLOW_LOAD_A(RA, G)                                                                                          \
   _Pragma("unroll") for (int s_ = 0; s_ < APER; ++s_) {                                                              \
     if constexpr (AIN == kInF32) /* rows of cin floats: channels past cin re-read the row's last 16 B (zeroed) */   \
@@ -209,9 +212,9 @@ __global__ __launch_bounds__(kThreads, 2) void conv_s32_kernel(ConvArgs a) {
   }
 #define OFLOW_WRITE_A(RA, BUF, G)                                                                                    \
   _Pragma("unroll") for (int s_ = 0; s_ < APER; ++s_) {                                                              \
-    const int item = tid + s_ * kThreads;                                                                            \
+    const int item = tid + s_ * NTH;                                                                            \
     const int p = item >> 3, c = item & 7;                                                                           \
-    if (AITEMS % kThreads == 0 || item < AITEMS) {                                                                   \
+    if (AITEMS % NTH == 0 || item < AITEMS) {                                                                   \
       if constexpr (AIN != kInS32) {                                                                                 \
         /* 4 fp32 channels (G*32 + 4c ..) [-> relu(x * scale + shift)] -> 4 hi + 4 lo halves (8 B each) */           \
         typedef _Float16 half4_ __attribute__((ext_vector_type(4)));                                                 \
@@ -225,30 +228,32 @@ __global__ __launch_bounds__(kThreads, 2) void conv_s32_kernel(ConvArgs a) {
               v_ = v_ * af.x + af.y;                                                                                 \
               v_ = v_ < 0.f ? 0.f : v_;                                                                              \
             }                                                                                                        \
-            const _Float16 hv = static_cast<_Float16>(v_);                                                           \
+            _Float16 hv, lv;                                                                                         \
+            split_f16(v_, hv, lv);                                                                                   \
             h4[e_] = hv;                                                                                             \
-            l4[e_] = static_cast<_Float16>(v_ - static_cast<float>(hv));                                             \
+            l4[e_] = lv;                                                                                             \
           }                                                                                                          \
         }                                                                                                            \
         uint8_t* rw_ = sA + (BUF) * A_BYTES + p * RS + (c & 1) * 8;                                                  \
         *reinterpret_cast<half4_*>(rw_ + (((c >> 1) ^ swz(p)) << 4)) = h4;                                           \
         *reinterpret_cast<half4_*>(rw_ + (((4 + (c >> 1)) ^ swz(p)) << 4)) = l4;                                     \
       } else {                                                                                                       \
-        *reinterpret_cast<u32x4*>(sA + (BUF) * A_BYTES + p * RS + ((c ^ swz(p)) << 4)) = RA[s_];                    \
+        *reinterpret_cast<u32x4*>(sA + (BUF) * A_BYTES + p * RS + ((c ^ swz(p)) << 4)) =                            \
+            ((aok >> s_) & 1u) ? RA[s_] : u32x4{0u, 0u, 0u, 0u};                                                     \
       }                                                                                                              \
     }                                                                                                                \
   }
 #define OFLOW_LOAD_B(RB, STEP)                                                                                       \
   _Pragma("unroll") for (int s_ = 0; s_ < BPER; ++s_) {                                                              \
-    const int item = tid + s_ * kThreads;                                                                            \
-    if (BITEMS % kThreads == 0 || item < BITEMS)                                                                     \
+    const int item = tid + s_ * NTH;                                                                            \
+    if (BITEMS % NTH == 0 || item < BITEMS)                                                                     \
       RB[s_] = __builtin_amdgcn_raw_buffer_load_b128(rsB, boff[s_], (STEP) * a.npad * 128, 0);                      \
   }
 #define OFLOW_WRITE_B(RB, BUF)                                                                                       \
   _Pragma("unroll") for (int s_ = 0; s_ < BPER; ++s_) {                                                              \
-    const int item = tid + s_ * kThreads;                                                                            \
+    const int item = tid + s_ * NTH;                                                                            \
     const int n = item >> 3, c = item & 7;                                                                           \
-    if (BITEMS % kThreads == 0 || item < BITEMS)                                                                     \
+    if (BITEMS % NTH == 0 || item < BITEMS)                                                                     \
       *reinterpret_cast<u32x4*>(sB + (BUF) * B_BYTES + n * RS + ((c ^ swz(n)) << 4)) = RB[s_];                      \
   }
   // operands of one 16-deep sub-step S_ of step I: A rows of this wave's pixel tiles at the step's tap offset, B rows
@@ -292,7 +297,7 @@ __global__ __launch_bounds__(kThreads, 2) void conv_s32_kernel(ConvArgs a) {
 
   const int S = a.kg * T;
   if constexpr (AIN == kInF32Norm) {
-    for (int e = tid; e < a.kg * 32; e += kThreads)
+    for (int e = tid; e < a.kg * 32; e += NTH)
       sAff[e] = make_float2(a.ia[(long long)b * a.kg * 32 + e], a.ib[(long long)b * a.kg * 32 + e]);
     __syncthreads();
   }
@@ -356,6 +361,7 @@ __global__ __launch_bounds__(kThreads, 2) void conv_s32_kernel(ConvArgs a) {
 #undef OFLOW_WRITE_B
 
   // ---- epilogue: accumulators -> LDS tile [pixel][channel] ----
+  __syncthreads();  // the tile overwrites the operand buffers: every wave is past its last LDS operand read
   float* sT = reinterpret_cast<float*>(smem);
 #pragma unroll
   for (int mt = 0; mt < MT; ++mt)
@@ -373,7 +379,7 @@ __global__ __launch_bounds__(kThreads, 2) void conv_s32_kernel(ConvArgs a) {
 
   if (a.f != nullptr) {
     // fp32 NCHW: lanes = consecutive pixels of one tile row (128-B rows of the destination)
-    for (int item = tid; item < BM * BN; item += kThreads) {
+    for (int item = tid; item < BM * BN; item += NTH) {
       const int nl = item / BM, pl = item - nl * BM;
       const int n = n0 + nl;
       const int y = ty0 + pl / kTX, x = tx0 + (pl % kTX);
@@ -394,7 +400,7 @@ __global__ __launch_bounds__(kThreads, 2) void conv_s32_kernel(ConvArgs a) {
       // per-tile instance-norm partials of the conv output (merged by oflow_norm_stats_finalize): SL = 256 / BN
       // adjacent lanes share a channel and take interleaved slices of the tile's pixels (two-pass mean / M2 in
       // fp32); the slices are merged across those lanes with xor shuffles (Chan et al.).
-      constexpr int SL = kThreads / BN >= 4 ? 4 : kThreads / BN >= 2 ? 2 : 1;
+      constexpr int SL = NTH / BN >= 4 ? 4 : NTH / BN >= 2 ? 2 : 1;
       const int c = tid / SL, sl = tid % SL;
       const int n = n0 + c;
       const bool on = c < BN && n < a.N;
@@ -453,7 +459,7 @@ __global__ __launch_bounds__(kThreads, 2) void conv_s32_kernel(ConvArgs a) {
 
   // S32 / GRU consumers: one thread = one pixel x 8 consecutive channels
   constexpr int C8 = BN / 8;
-  for (int item = tid; item < BM * C8; item += kThreads) {
+  for (int item = tid; item < BM * C8; item += NTH) {
     const int pl = item / C8, c8 = item - pl * C8;
     const int nl = c8 * 8, n = n0 + nl;
     const int y = ty0 + pl / kTX, x = tx0 + (pl % kTX);
@@ -539,18 +545,18 @@ int launch_conv(const ConvArgs& a0, hipStream_t s) {
   dim3 grid(a.tiles_x * a.tiles_y * a.B, a.npad / BN);
   if constexpr (KH == 3 && KW == 3 && EPI == 0) {  // the encoders' second block convs
     if (a.ain == kInF32Norm) {
-      hipLaunchKernelGGL((conv_s32_kernel<KH, KW, BN, WM, WN, EPI, TY, kInF32Norm>), grid, dim3(kThreads), 0, s, a);
+      hipLaunchKernelGGL((conv_s32_kernel<KH, KW, BN, WM, WN, EPI, TY, kInF32Norm>), grid, dim3(64 * WM * WN), 0, s, a);
       return launch_status();
     }
   }
   if constexpr (KH == 1 && KW == 1 && EPI == 0 && BN == 128) {  // convc1 on the NHWC corr lookup
     if (a.ain == kInF32) {
-      hipLaunchKernelGGL((conv_s32_kernel<KH, KW, BN, WM, WN, EPI, TY, kInF32>), grid, dim3(kThreads), 0, s, a);
+      hipLaunchKernelGGL((conv_s32_kernel<KH, KW, BN, WM, WN, EPI, TY, kInF32>), grid, dim3(64 * WM * WN), 0, s, a);
       return launch_status();
     }
   }
   if (a.ain != kInS32) return OFLOW_E_MODE;
-  hipLaunchKernelGGL((conv_s32_kernel<KH, KW, BN, WM, WN, EPI, TY>), grid, dim3(kThreads), 0, s, a);
+  hipLaunchKernelGGL((conv_s32_kernel<KH, KW, BN, WM, WN, EPI, TY>), grid, dim3(64 * WM * WN), 0, s, a);
   return launch_status();
 }
 

@@ -29,9 +29,10 @@ __device__ __forceinline__ void put8(uint8_t* line, const float* v) {
   half8 hi, lo;
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
-    const _Float16 a = static_cast<_Float16>(v[j]);
-    hi[j] = a;
-    lo[j] = static_cast<_Float16>(v[j] - static_cast<float>(a));
+    _Float16 h_, l_;
+    split_f16(v[j], h_, l_);
+    hi[j] = h_;
+    lo[j] = l_;
   }
   *reinterpret_cast<half8*>(line) = hi;
   *reinterpret_cast<half8*>(line + 64) = lo;
@@ -88,8 +89,9 @@ __global__ __launch_bounds__(256) void stem_patches_kernel(const float* __restri
     half8 h;
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
-      const _Float16 a = static_cast<_Float16>(v[e]);
-      h[e] = piece < 4 ? a : static_cast<_Float16>(v[e] - static_cast<float>(a));
+      _Float16 h_, l_;
+      split_f16(v[e], h_, l_);
+      h[e] = piece < 4 ? h_ : l_;
     }
     *reinterpret_cast<half8*>(dst + (long long)line * 128 + (piece < 4 ? q * 16 : 64 + q * 16)) = h;
   }

@@ -27,6 +27,19 @@ __device__ __forceinline__ float pool4(float a, float b, float c, float d) {
   return s * 0.25f;
 }
 
+// fp32 -> split fp16 pair (hi, lo): hi = fp16(v), lo = fp16(v - hi), so hi + lo holds v to ~22 bits (the S32 format).
+// v is pinned to a VGPR first (empty asm) and contraction is off: otherwise the multiply that produced v (the GRU
+// epilogue's r * h) is folded into the conversions -- hi as v_fma_mix (fp16(r * h), one rounding) and the residual
+// from a second, double-rounded fp16(fp32(r * h)) -- and where the two roundings differ hi + lo is one fp16 ulp off
+// (seen at 2 of 9216 elements, tests/test_gpu_conv_s32.py::test_conv_s32_gru_epilogues).
+__device__ __forceinline__ void split_f16(float v, _Float16& hi, _Float16& lo) {
+#pragma clang fp contract(off)
+  asm volatile("" : "+v"(v));
+  const _Float16 a = static_cast<_Float16>(v);
+  hi = a;
+  lo = static_cast<_Float16>(v - static_cast<float>(a));
+}
+
 inline int launch_status() {
   hipError_t e = hipGetLastError();
   return e == hipSuccess ? OFLOW_OK : static_cast<int>(e);

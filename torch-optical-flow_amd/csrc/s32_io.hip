@@ -25,9 +25,10 @@ __device__ __forceinline__ void put8(uint8_t* line, const float* v) {
   half8 hi, lo;
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
-    const _Float16 a = static_cast<_Float16>(v[j]);
-    hi[j] = a;
-    lo[j] = static_cast<_Float16>(v[j] - static_cast<float>(a));
+    _Float16 h_, l_;
+    split_f16(v[j], h_, l_);
+    hi[j] = h_;
+    lo[j] = l_;
   }
   *reinterpret_cast<half8*>(line) = hi;
   *reinterpret_cast<half8*>(line + 64) = lo;
@@ -102,9 +103,9 @@ __global__ __launch_bounds__(256) void flow_prep_kernel(const float* __restrict_
   for (int c = 0; c < 4; ++c) put8(line + c * 16, v + 8 * c);
   if (g == 0 && d0) {
     const float fx = cx[pix] - static_cast<float>(x), fy = cy[pix] - static_cast<float>(y);
-    const _Float16 hx = static_cast<_Float16>(fx), hy = static_cast<_Float16>(fy);
-    const _Float16 lx = static_cast<_Float16>(fx - static_cast<float>(hx));
-    const _Float16 ly = static_cast<_Float16>(fy - static_cast<float>(hy));
+    _Float16 hx, lx, hy, ly;
+    split_f16(fx, hx, lx);
+    split_f16(fy, hy, ly);
     for (int d = 0; d < 2; ++d) {
       uint8_t* dst = d == 0 ? d0 + p * d0ps : (d1 ? d1 + p * d1ps : nullptr);
       if (!dst) continue;
