@@ -37,6 +37,7 @@ import torch.distributed as dist  # noqa: E402
 METRIC = "image-pairs/sec + corr-lookup HBM GB/s, RAFT 12-iter @ Sintel 1024×436"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 MFMA_F32_PEAK_TFLOPS = 157.3  # dense fp32 MFMA (v_mfma_f32_32x32x2_f32), spec
+MFMA_F16_PEAK_TFLOPS = 2500.0  # dense fp16 MFMA, spec (no sparsity)
 PMC_TRAFFIC_FILE = os.path.join(REPO, "profiles", "lookup_traffic.json")
 
 WORKLOADS = {
@@ -65,6 +66,50 @@ def pyramid_cost(batch: int, dims, c: int = 256):
     write = batch * n * sum(h * w for h, w in dims) * 4
     read = 2 * batch * n * c * 4
     return flops, write + read
+
+
+def fused_lookup_bytes(batch: int, dims, lanes: int, radius: int = 4) -> int:
+    """Algorithmic HBM bytes of the fused lookup + convc1 per iteration over ``batch`` pairs in ``lanes`` launches:
+    per query the lookup's window reads (SURVEY §8(d) term 1) + its coordinates (8 B) + the S32 output (256 channels
+    x 4 B); per launch the level-regrouped weights (L * G k32 groups x 256 channels x 128 B)."""
+    h0, w0 = dims[0]
+    p = 2 * radius + 2
+    g = ((2 * radius + 1) ** 2 + 31) // 32
+    per_q = sum(min(p, h) * min(p, w) * 4 for h, w in dims) + 8 + 256 * 4
+    return batch * h0 * w0 * per_q + lanes * len(dims) * g * 256 * 128
+
+
+def fused_lookup_flops(batch: int, dims, radius: int = 4) -> int:
+    """Executed f16 MFMA flops of the fused kernel per iteration: queries x (L * G * 32) x 256 x 2 x 3 split products."""
+    g = ((2 * radius + 1) ** 2 + 31) // 32
+    return batch * dims[0][0] * dims[0][1] * len(dims) * g * 32 * 256 * 2 * 3
+
+
+def pmc_traffic(workload: str, ppg: int, kernel: str):
+    """HBM bytes per launch of ``kernel`` measured by rocprofv3 PMC (FETCH_SIZE + WRITE_SIZE, the guide's gfx950
+    corrections) on this build, as recorded in profiles/lookup_traffic.json by tools/pmc_traffic.py; None if absent."""
+    if not os.path.exists(PMC_TRAFFIC_FILE):
+        return None
+    with open(PMC_TRAFFIC_FILE) as f:
+        tr = json.load(f).get(f"{workload}:{ppg}:{kernel}")
+    return tr.get("hbm_bytes_per_launch") if tr else None
+
+
+def pyramid_entry(pk, ppg: int, dims):
+    pk_ms = mean_ms(pk)
+    flops, nbytes = pyramid_cost(ppg, dims)
+    tf = flops / (pk_ms * 1e-3) / 1e12
+    return {
+        "bound": "mfma",
+        "note": "in-step: runs beside cnet (side stream); alone: tools/kbench.py",
+        "launch_ms": round(pk_ms, 4),
+        "achieved_tflops": round(tf, 2),
+        "peak_tflops": MFMA_F32_PEAK_TFLOPS,
+        "frac": round(tf / MFMA_F32_PEAK_TFLOPS, 4),
+        "hbm_gbs": round(nbytes / (pk_ms * 1e-3) / 1e9, 1),
+        "flops_per_launch": flops,
+        "bytes_per_launch": nbytes,
+    }
 
 
 def mean_ms(events) -> float:
@@ -314,6 +359,33 @@ def main() -> int:
             "corr_lookup_otf": {"launch_ms": round(mean_ms(lk), 4), "launches": len(lk)},
             "corr_otf_prepare": {"launch_ms": round(mean_ms(pp), 4) if pp else None},
         }
+    elif rec and rec.get("corr_lookup_convc1"):
+        # the RAFT forward's lookup runs inside convc1 (csrc/corr_convc1.hip): one launch per lane per iteration
+        lk = rec["corr_lookup_convc1"]
+        pk = rec.get("corr_pyramid", [])
+        lk_ms = mean_ms(lk)
+        lanes = max(1, len(lk) // (iters * args.steps))
+        lk_bytes = fused_lookup_bytes(ppg, dims, lanes) // lanes
+        flops = fused_lookup_flops(ppg, dims) // lanes
+        ach = lk_bytes / (lk_ms * 1e-3) / 1e9
+        tf = flops / (lk_ms * 1e-3) / 1e12
+        line["roofline"] = {
+            "kernel": "corr_lookup_convc1 (the windowed lookup fused into convc1: gathers from the tiled pyramid, "
+            "split-fp16 MFMA 1x1 conv, ReLU, S32 out; the lookup volume never reaches HBM)",
+            "bound": "hbm",
+            "achieved": round(ach, 1),
+            "peak": HBM_PEAK_GBS,
+            "unit": "GB/s",
+            "frac": round(ach / HBM_PEAK_GBS, 4),
+            "traffic": pmc_traffic(args.workload, ppg, "corr_lookup_convc1"),
+            "algorithmic_bytes_per_launch": lk_bytes,
+            "launch_ms": round(lk_ms, 5),
+            "launches": len(lk),
+            "mfma": {"executed_f16_tflops": round(tf, 1), "peak_tflops": MFMA_F16_PEAK_TFLOPS,
+                     "frac": round(tf / MFMA_F16_PEAK_TFLOPS, 4), "flops_per_launch": flops},
+        }
+        if pk:
+            line["kernels"] = {"corr_pyramid": pyramid_entry(pk, ppg, dims)}
     elif rec and rec.get("corr_lookup"):
         lk = rec.get("corr_lookup", [])
         pk = rec.get("corr_pyramid", [])
@@ -321,11 +393,7 @@ def main() -> int:
         # per launch: a step does `iters` full-batch lookups' worth of queries over len(lk)/steps launches
         lk_bytes = lookup_bytes(ppg, dims) * iters * args.steps // max(1, len(lk))
         ach = lk_bytes / (lk_ms * 1e-3) / 1e9
-        traffic = None
-        if os.path.exists(PMC_TRAFFIC_FILE):
-            with open(PMC_TRAFFIC_FILE) as f:
-                tr = json.load(f).get(f"{args.workload}:{ppg}")
-            traffic = tr.get("hbm_bytes_per_launch") if tr else None
+        traffic = pmc_traffic(args.workload, ppg, "corr_lookup")
         line["roofline"] = {
             "kernel": "corr_lookup" + ("_tiled_nhwc (RAFT forward: fp32 NHWC rows, convc1's input)"
                                        if args.workload != "corr" and args.update_impl == "split" else ""),
@@ -340,22 +408,7 @@ def main() -> int:
             "launches": len(lk),
         }
         if pk:
-            pk_ms = mean_ms(pk)
-            flops, nbytes = pyramid_cost(ppg, dims)
-            tf = flops / (pk_ms * 1e-3) / 1e12
-            line["kernels"] = {
-                "corr_pyramid": {
-                    "bound": "mfma",
-                    "note": "in-step: runs beside cnet (side stream); alone: tools/kbench.py",
-                    "launch_ms": round(pk_ms, 4),
-                    "achieved_tflops": round(tf, 2),
-                    "peak_tflops": MFMA_F32_PEAK_TFLOPS,
-                    "frac": round(tf / MFMA_F32_PEAK_TFLOPS, 4),
-                    "hbm_gbs": round(nbytes / (pk_ms * 1e-3) / 1e9, 1),
-                    "flops_per_launch": flops,
-                    "bytes_per_launch": nbytes,
-                }
-            }
+            line["kernels"] = {"corr_pyramid": pyramid_entry(pk, ppg, dims)}
     if epe is not None:
         line["epe_vs_reference"] = {k: (round(v, 8) if isinstance(v, float) else v) for k, v in epe.items()}
     if rank == 0 and world == 1 and not args.no_cpu_baseline and args.workload in ("sintel", "kitti"):

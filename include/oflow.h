@@ -192,6 +192,16 @@ int oflow_flow_prep_s32(const float* d_coords, int B, int H, int W, void* d_patc
 int oflow_corr_lookup_tiled_nhwc_f32(const float* const* d_levels, const int* level_h, const int* level_w, int num_levels,
                                      const float* d_coords, int B, int H, int W, int radius, float* d_out, int row_floats,
                                      void* stream);
+/* oflow_corr_lookup_convc1_s32: the tiled lookup fused into the motion encoder's first convolution -- S32 output
+ * y = relu(convc1(corr_fn(coords))) (256 channels: d_y + P * y_pixel_stride, 8 groups), the lookup volume never
+ * written. Replaces raft.py:128 (corr.py:56-77) + update.py:120-121 (`F.relu(self.convc1(corr))`) in the forward.
+ * Weights: oflow_conv_s32's packing (1x1, n_pad 256) of convc1 with its input channels regrouped per level -- level l's
+ * tap k at channel l*G*32 + k, G = ceil((2r+1)^2/32), zeros elsewhere (num_levels*G groups); d_wscale [256], d_bias [256]
+ * or NULL. radius 3 or 4 (else OFLOW_E_RADIUS), y_pixel_stride % 128 == 0. */
+int oflow_corr_lookup_convc1_s32(const float* const* d_levels, const int* level_h, const int* level_w, int num_levels,
+                                 const float* d_coords, int B, int H, int W, int radius, const void* d_wpack,
+                                 const float* d_wscale, const float* d_bias, void* d_y, long long y_pixel_stride,
+                                 void* stream);
 
 /*
  * Encoders on the split-fp16 path (methods/raft/model/extractor.py:35-231; csrc/encoder_s32.hip).

@@ -156,6 +156,9 @@ __global__ __launch_bounds__(64 * WM * WN, WM * WN == 8 ? 1 : 2) void conv_s32_k
   constexpr int LDS_BYTES = MAIN_BYTES > EPI_BYTES ? MAIN_BYTES : EPI_BYTES;
   constexpr int AFF_BYTES = AIN == kInF32Norm ? kAinGroups * 32 * 8 : 0;  // float2 (scale, shift) per input channel
   __shared__ __attribute__((aligned(16))) uint8_t smem[LDS_BYTES + AFF_BYTES];
+  // the block's per-channel (inverse weight scale, bias), staged once for the epilogue (whose loops would otherwise
+  // wait on a global-load round trip per iteration)
+  __shared__ float2 sSB[BN];
   float2* sAff = reinterpret_cast<float2*>(smem + LDS_BYTES);
   uint8_t* sA = smem;
   uint8_t* sB = smem + (ADB ? 2 : 1) * A_BYTES;
@@ -296,6 +299,10 @@ __global__ __launch_bounds__(64 * WM * WN, WM * WN == 8 ? 1 : 2) void conv_s32_k
       for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
 
   const int S = a.kg * T;
+  for (int c = tid; c < BN; c += NTH) {
+    const int n = min(n0 + c, a.N - 1);
+    sSB[c] = make_float2(a.wsc[n], a.bias ? a.bias[n] : 0.f);
+  }
   if constexpr (AIN == kInF32Norm) {
     for (int e = tid; e < a.kg * 32; e += NTH)
       sAff[e] = make_float2(a.ia[(long long)b * a.kg * 32 + e], a.ib[(long long)b * a.kg * 32 + e]);
@@ -384,8 +391,8 @@ __global__ __launch_bounds__(64 * WM * WN, WM * WN == 8 ? 1 : 2) void conv_s32_k
       const int n = n0 + nl;
       const int y = ty0 + pl / kTX, x = tx0 + (pl % kTX);
       if (n < a.N && y < a.H && x < a.W) {
-        float v = sT[pl * TS + nl] * a.wsc[n];
-        if (a.bias) v += a.bias[n];
+        const float2 sb = sSB[nl];
+        float v = sT[pl * TS + nl] * sb.x + sb.y;
         v = act_fn(v, a.act) * a.oscale;
         float* d = a.f + b * a.fbs + n * a.fcs + (long long)y * a.W + x;
         if (a.faccum)
@@ -404,7 +411,7 @@ __global__ __launch_bounds__(64 * WM * WN, WM * WN == 8 ? 1 : 2) void conv_s32_k
       const int c = tid / SL, sl = tid % SL;
       const int n = n0 + c;
       const bool on = c < BN && n < a.N;
-      const float ws = on ? a.wsc[n] : 0.f, bi = (on && a.bias) ? a.bias[n] : 0.f;
+      const float ws = on ? sSB[c].x : 0.f, bi = on ? sSB[c].y : 0.f;
       int cnt = 0;
       float sum = 0.f;
       if (on) {
@@ -470,8 +477,8 @@ __global__ __launch_bounds__(64 * WM * WN, WM * WN == 8 ? 1 : 2) void conv_s32_k
     float v[8] = {t0.x, t0.y, t0.z, t0.w, t1.x, t1.y, t1.z, t1.w};
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-      const int nj = n + j < a.N ? n + j : a.N - 1;
-      v[j] = v[j] * a.wsc[nj] + (a.bias ? a.bias[nj] : 0.f);
+      const float2 sb = sSB[nl + j];
+      v[j] = v[j] * sb.x + sb.y;
     }
     if constexpr (EPI == 0) {
 #pragma unroll

@@ -20,11 +20,6 @@ namespace {
 constexpr int kQ = 64;  // queries per workgroup (canonical kernel)
 constexpr int kThreads = 256;
 
-// nw*w.x + ne*w.y + sw*w.z + se*w.w in one fixed rounding order (so that every lookup kernel agrees bit for bit)
-__device__ __forceinline__ float bilinear4(float nw, float ne, float sw, float se, float4 w) {
-  return fmaf(se, w.w, fmaf(sw, w.z, fmaf(ne, w.y, __fmul_rn(nw, w.x))));
-}
-
 struct LookupArgs {
   const float* lv[OFLOW_MAX_LEVELS];
   int nqb;              // query blocks

@@ -40,6 +40,31 @@ __device__ __forceinline__ void split_f16(float v, _Float16& hi, _Float16& lo) {
   lo = static_cast<_Float16>(v - static_cast<float>(a));
 }
 
+// Bilinear tap of the lookup: nw*w.x + ne*w.y + sw*w.z + se*w.w in one fixed rounding order, shared by every lookup
+// kernel (corr_lookup.hip, corr_convc1.hip) so that they agree bit for bit.
+__device__ __forceinline__ float bilinear4(float nw, float ne, float sw, float se, float4 w) {
+  return fmaf(se, w.w, fmaf(sw, w.z, fmaf(ne, w.y, __fmul_rn(nw, w.x))));
+}
+
+// Window origin and bilinear weights of one (query, level) (corr.py:63-70 in pixel space): centre
+// c = coords / 2^l; origin floor(c) - r; weights (nw, ne, sw, se) as grid_sample's CPU kernel forms them. |c| >= 2^22
+// (or NaN / inf) puts every tap far outside any level: origin far away, all-zero window.
+__device__ __forceinline__ void window_origin(float cx, float cy, float inv, int r, int& xs, int& ys, float4& w) {
+  cx *= inv;
+  cy *= inv;
+  xs = -(1 << 28);
+  ys = -(1 << 28);
+  w = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (fabsf(cx) < 4194304.0f && fabsf(cy) < 4194304.0f) {
+    const float fx = floorf(cx), fy = floorf(cy);
+    const float wx = cx - fx, wy = cy - fy;  // exact
+    const float ex = 1.0f - wx, ey = 1.0f - wy;
+    xs = static_cast<int>(fx) - r;
+    ys = static_cast<int>(fy) - r;
+    w = make_float4(ey * ex, ey * wx, wy * ex, wy * wx);
+  }
+}
+
 inline int launch_status() {
   hipError_t e = hipGetLastError();
   return e == hipSuccess ? OFLOW_OK : static_cast<int>(e);

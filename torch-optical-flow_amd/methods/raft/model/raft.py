@@ -102,6 +102,9 @@ class RAFT(nn.Module):
         # lookup per iteration on the main stream (both halves joined around it); "lane": each half looks up its own.
         self.pair_lanes = 2
         self.pair_lookup = "joined"
+        # lookup fused into convc1 (csrc/corr_convc1.hip; CorrBlock, radius 3 / 4): each lane runs
+        # relu(convc1(lookup)) as one kernel and the lookup volume never reaches HBM (pair_lookup then does not apply)
+        self.lookup_fusion = True
         # the split paths cache packed fp16 hi/lo weights keyed by (storage, version); parameters created under
         # torch.inference_mode() have no version counter, so loading new weights in place drops the caches
         for m in (self.fnet, self.cnet, self.update_block):
@@ -167,14 +170,17 @@ class RAFT(nn.Module):
         cuts = list(zip(edges[:-1], edges[1:]))
         main = torch.cuda.current_stream(dev)
         lanes = [main] + [_side_stream(dev, 100 + i) for i in range(1, n)]
+        # the packed weights (built on first use, by kernels on this stream) must exist before the lanes fork: the
+        # lanes read them with no later join when the lookup is not joined (fused into convc1, or pair_lookup "lane")
+        SplitUpdate._weights(self.update_block)
         for st in lanes[1:]:
             st.wait_stream(main)
         runners = []
         for i, ((b0, b1), st) in enumerate(zip(cuts, lanes)):
             with torch.cuda.stream(st):
                 slot = 0 if i == 0 else 200 + i
-                runners.append(SplitUpdate(self.update_block, cnet_out[b0:b1], hdim, side_slot=slot))
-        joined = self.pair_lookup == "joined"
+                runners.append(SplitUpdate(self.update_block, cnet_out[b0:b1], hdim, side_slot=slot, fuse_c1=self.lookup_fusion))
+        joined = self.pair_lookup == "joined" and not runners[0].fusable(corr_fn)
         hw = cnet_out.shape[2] * cnet_out.shape[3]
         if joined:
             rows = torch.empty((b * hw, runners[0].corr_ch), device=dev, dtype=torch.float32)
@@ -270,7 +276,7 @@ class RAFT(nn.Module):
             return flow_predictions
         if impl == "split":
             # coords1 is advanced in place by the flow head's epilogue (raft.py:133)
-            runner = SplitUpdate(self.update_block, cnet_out, hdim)
+            runner = SplitUpdate(self.update_block, cnet_out, hdim, fuse_c1=self.lookup_fusion)
             coords1 = coords1.contiguous()
             for itr in range(iters):
                 last = itr == iters - 1

@@ -3,7 +3,7 @@
 The ``nn.Module`` classes restate the reference's layers (same parameter names, so checkpoints load); they are
 what autograd / CPU runs use. GPU inference runs ``SplitUpdate``: every convolution on the split-fp16 matrix-core
 kernel (csrc/conv_s32.hip) with the GRU gates, activations, concatenations and the coords update fused into
-convolution epilogues; convc1 reads the lookup's fp32 NHWC rows directly (split into hi + lo while staged).
+convolution epilogues; the correlation lookup runs inside convc1 (csrc/corr_convc1.hip).
 ``FusedUpdate`` (MIOpen convolutions + fused elementwise kernels) is kept for A/B runs. ``ConvGRU`` (unused by RAFT)
 is not provided.
 """
@@ -161,6 +161,15 @@ class FusedUpdate:
         return net, mask, delta_flow
 
 
+class FusedLookup:
+    """convc1's input when the lookup runs inside it: the tiled pyramid, the coordinates and the radius."""
+
+    __slots__ = ("pyr", "coords", "radius")
+
+    def __init__(self, pyr, coords: Tensor, radius: int) -> None:
+        self.pyr, self.coords, self.radius = pyr, coords, radius
+
+
 _SIDE_STREAMS = {}
 
 
@@ -194,13 +203,15 @@ class SplitUpdate:
       rhx = [r*h | inp | motion | flow]          (GRU input of the candidate)      12 groups
       cf  = [relu(convc2) (192) | relu(convf2) (64)]  (input of the motion conv)  8 groups
     h is also kept in fp32 ([P, 128]) so that the blend h = (1-z)h + zq (`update.py:97`) runs in fp32.
-    Per iteration: lookup -> corr (S32), flow_prep -> flow channels + convf1's 7x7 patch matrix, then
-    convc1, convc2, convf1 (1x1 over the patches), convf2, conv (-> hx, rhx), [z|r] (-> z, r*h -> rhx),
+    Per iteration: the lookup fused into convc1 (oflow_corr_lookup_convc1_s32: the lookup volume is never written;
+    otherwise lookup -> fp32 NHWC rows -> convc1), flow_prep -> flow channels + convf1's 7x7 patch matrix, then
+    convc2, convf1 (1x1 over the patches), convf2, conv (-> hx, rhx), [z|r] (-> z, r*h -> rhx),
     q (-> h, hx) for the 1x5 and the 5x1 half, flow head conv1, conv2 (coords1 += delta in its epilogue), and at the
     last iteration the mask head (1x1 conv 256 -> 576 with the x0.25 in its epilogue, fp32 NCHW).
     """
 
-    def __init__(self, block: BasicUpdateBlock, cnet_out: Tensor, hdim: int, side_slot: int = 0) -> None:
+    def __init__(self, block: BasicUpdateBlock, cnet_out: Tensor, hdim: int, side_slot: int = 0,
+                 fuse_c1: bool = True) -> None:
         b, c, h, w = cnet_out.shape
         enc, gru = block.encoder, block.gru
         cdim = c - hdim
@@ -225,6 +236,7 @@ class SplitUpdate:
         _native.pack_s32(cnet_out[:, :hdim], "tanh", V(self.hx, 0, 4), nhwc=self.hm)  # raft.py:117
         _native.pack_s32(cnet_out[:, hdim:], "relu", V(self.hx, 4, 4), V(self.rhx, 4, 4))  # raft.py:118
         self.w = self._weights(block)
+        self.fuse_c1 = fuse_c1 and "c1L" in self.w
         # side stream for the motion encoder's flow branch (one per device, reused across forwards)
         self.streams = getattr(block, "split_streams", True)
         self.side_stream = _side_stream(dev, side_slot) if self.streams else None
@@ -248,6 +260,8 @@ class SplitUpdate:
             "m1": CW(block.mask[0].weight, block.mask[0].bias, 256),
             "m2": CW(block.mask[2].weight, block.mask[2].bias, 576),
         }
+        if block.corr_radius in (3, 4):  # the lookup fused into convc1 (corr_convc1.hip): weights regrouped per level
+            w["c1L"] = _native.convc1_level_weights(enc.convc1, block.corr_levels, block.corr_radius)
         for tag in ("1", "2"):
             cz, cr, cq = (getattr(gru, f"conv{g}{tag}") for g in "zrq")
             w["zr" + tag] = CW(torch.cat([cz.weight, cr.weight]), torch.cat([cz.bias, cr.bias]), 256)
@@ -267,11 +281,25 @@ class SplitUpdate:
             self.corr_f32 = torch.empty((b * h * wd, self.corr_ch), device=coords1.device, dtype=torch.float32)
         return self.corr_f32
 
+    def fusable(self, corr_fn) -> bool:
+        """Whether convc1 takes its input straight from ``corr_fn``'s tiled pyramid (oflow_corr_lookup_convc1_s32)."""
+        return self.fuse_c1 and getattr(corr_fn, "_tiled", None) is not None and corr_fn.radius in (3, 4)
+
     def lookup(self, corr_fn, coords1: Tensor):
-        """The correlation lookup as convc1's input (`raft.py:128`): fp32 NHWC rows, split while convc1 stages them."""
+        """The correlation lookup as convc1's input (`raft.py:128`): the tiled pyramid itself when the lookup runs
+        inside convc1 (``FusedLookup``), else fp32 NHWC rows split while convc1 stages them."""
+        if self.fusable(corr_fn):
+            return FusedLookup(corr_fn._tiled, coords1, corr_fn.radius)
         b, h, wd = self.shape
         corr_fn.lookup_nhwc(coords1, self.lookup_rows(coords1))
         return _native.F32In(self.corr_f32, b, h, wd)
+
+    def _convc1(self, corr_in) -> None:
+        """relu(convc1(corr)) -> c1 (`update.py:120`)."""
+        if isinstance(corr_in, FusedLookup):
+            _native.corr_lookup_convc1(corr_in.pyr, corr_in.coords, corr_in.radius, self.w["c1L"], _native.S32Slice(self.c1))
+        else:
+            _native.conv_s32(corr_in, self.w["c1"], 128, "relu", y0=_native.S32Slice(self.c1))
 
     def update(self, corr_in, coords1: Tensor, need_mask: bool, mask_out: Optional[Tensor] = None) -> Optional[Tensor]:
         """Everything of one update after the lookup; ``corr_in`` is convc1's input (F32In)."""
@@ -290,12 +318,12 @@ class SplitUpdate:
                 _native.flow_prep(coords1, self.pm, (V(self.hx), 382), (V(self.rhx), 382))
                 conv(V(self.pm), w["f1"], 128, "relu", y0=V(self.f1))
                 conv(V(self.f1), w["f2"], 64, "relu", y0=V(self.cf, 6, 2))
-            conv(corr_in, w["c1"], 128, "relu", y0=V(self.c1))
+            self._convc1(corr_in)
             conv(V(self.c1), w["c2"], 64, "relu", y0=V(self.cf, 0, 6))
             main.wait_stream(side)
         else:
             _native.flow_prep(coords1, self.pm, (V(self.hx), 382), (V(self.rhx), 382))
-            conv(corr_in, w["c1"], 128, "relu", y0=V(self.c1))
+            self._convc1(corr_in)
             conv(V(self.c1), w["c2"], 64, "relu", y0=V(self.cf, 0, 6))
             conv(V(self.pm), w["f1"], 128, "relu", y0=V(self.f1))
             conv(V(self.f1), w["f2"], 64, "relu", y0=V(self.cf, 6, 2))

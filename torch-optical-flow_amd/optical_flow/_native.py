@@ -61,6 +61,7 @@ SYMBOLS = (
     "oflow_flow_stats_f32",
     "oflow_flow2rgb_f32",
     "oflow_flow_pack_f32",
+    "oflow_corr_lookup_convc1_s32",
 )
 
 _lib = None
@@ -75,7 +76,7 @@ def set_event_recorder(recorder):
 
 
 # ops whose launches are bracketed by events when a recorder is set (others only if the recorder has "*": True)
-_TIMED_DEFAULT = ("corr_lookup", "corr_pyramid", "corr_lookup_otf", "corr_otf_prepare", "grid_warp")
+_TIMED_DEFAULT = ("corr_lookup", "corr_lookup_convc1", "corr_pyramid", "corr_lookup_otf", "corr_otf_prepare", "grid_warp")
 
 
 class _Timed:
@@ -176,6 +177,8 @@ def load() -> ctypes.CDLL:
     lib.oflow_corr_lookup_tiled_nhwc_f32.restype = I
     lib.oflow_corr_lookup_tiled_nhwc_f32.argtypes = [PP, IP, IP, I, P, I, I, I, I, P, I, P]
     lib.oflow_convex_upsample_f32.restype = I
+    lib.oflow_corr_lookup_convc1_s32.restype = I
+    lib.oflow_corr_lookup_convc1_s32.argtypes = [PP, IP, IP, I, P, I, I, I, I, P, P, P, P, ctypes.c_longlong, P]
     lib.oflow_convex_upsample_f32.argtypes = [P, P, I, I, I, P, P]
     lib.oflow_flow_stats_f32.restype = I
     lib.oflow_flow_stats_f32.argtypes = [P, I, I, I, I, F, F, I, P, P]
@@ -682,6 +685,48 @@ class ConvWeights:
         self.wscale = inv
         self.bias = None if bias is None else bias.detach().float().contiguous()
         self.n, self.n_pad, self.kh, self.kw, self.kg = n, n_pad, kh, kw, kg
+
+
+def convc1_level_weights(conv: torch.nn.Conv2d, num_levels: int, radius: int) -> "ConvWeights":
+    """convc1 (1x1, L*(2r+1)^2 -> 256) packed for oflow_corr_lookup_convc1_s32: input channel l*(2r+1)^2 + k (the
+    lookup's channel order, corr.py:71-77) moved to l*G*32 + k, G = ceil((2r+1)^2 / 32), zeros between levels."""
+    kk = (2 * radius + 1) ** 2
+    g = (kk + 31) // 32
+    w = conv.weight.detach().float()
+    if tuple(w.shape[1:]) != (num_levels * kk, 1, 1):
+        raise RuntimeError(f"convc1_level_weights: expected a 1x1 conv over {num_levels * kk} channels, got {tuple(w.shape)}")
+    wp = w.new_zeros((w.shape[0], num_levels * g * 32, 1, 1))
+    for l in range(num_levels):
+        wp[:, l * g * 32 : l * g * 32 + kk] = w[:, l * kk : (l + 1) * kk]
+    return ConvWeights(wp, conv.bias, w.shape[0])
+
+
+def corr_lookup_convc1(pyr: "TiledPyramid", coords: torch.Tensor, radius: int, cw: "ConvWeights", y: "S32Slice") -> None:
+    """relu(convc1(lookup(coords))) straight into the S32 slice ``y`` (256 channels), the lookup fused into the
+    convolution (oflow_corr_lookup_convc1_s32): the RAFT forward's `F.relu(self.convc1(corr_fn(coords1)))`
+    (raft.py:128, update.py:120-121). ``cw``: ``convc1_level_weights``."""
+    what = "corr_lookup_convc1"
+    co = _gpu_f32(coords, "coords", what)
+    b, two, h, w = co.shape
+    if two != 2 or b * h * w != pyr.queries:
+        raise RuntimeError(f"{what}: coords (B, 2, H, W) must cover the pyramid's {pyr.queries} queries")
+    kk = (2 * radius + 1) ** 2
+    if cw.n != 256 or cw.n_pad != 256 or cw.kh * cw.kw != 1 or cw.kg != len(pyr.levels) * ((kk + 31) // 32):
+        raise RuntimeError(f"{what}: weights must be convc1_level_weights of this pyramid / radius")
+    if y.ng != 8 or y.bhw != (b, h, w) or y.device != co.device:
+        raise RuntimeError(f"{what}: destination must be an 8-group S32 slice of shape ({b}, {h}, {w})")
+    n = len(pyr.levels)
+    ptrs = (ctypes.c_void_p * MAX_LEVELS)(*[t.data_ptr() for t in pyr.levels])
+    hs = (ctypes.c_int * MAX_LEVELS)(*[d[0] for d in pyr.dims])
+    ws = (ctypes.c_int * MAX_LEVELS)(*[d[1] for d in pyr.dims])
+    with torch.cuda.device(co.device), _Timed(what, co.device):
+        _check(
+            load().oflow_corr_lookup_convc1_s32(
+                ptrs, hs, ws, n, co.data_ptr(), b, h, w, int(radius), cw.pack.data_ptr(), cw.wscale.data_ptr(),
+                cw.bias.data_ptr() if cw.bias is not None else None, y.ptr, y.ps, _stream(co.device),
+            ),
+            what,
+        )
 
 
 def conv_tiles(h: int, w: int) -> int:
