@@ -188,19 +188,25 @@ __global__ __launch_bounds__(64 * WM * WN, WM * WN == 8 ? 1 : 2) void conv_s32_k
       const_cast<uint8_t*>(a.x + pix0 * a.xps), (short)0, (int)((long long)a.H * a.W * a.xps), 0x00020000);
   const __amdgpu_buffer_rsrc_t rsB =
       __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(a.w), (short)0, a.wbytes, 0x00020000);
-  int aoff[APER];
-  int acol[APER];  // kInF32: byte offset of the item's 4 channels within a 32-channel group (added per group, clamped)
+  // the halo item offsets are recomputed at each load from an opaque copy of tid (a few VALU per group) rather than
+  // kept in APER live registers (the 3x3 BN64 8-row variant spilled them to scratch inside the main loop)
+  auto a_off = [&](int s_, int& col) {
+    int t_ = tid;
+    asm volatile("" : "+v"(t_));
+    const int item = (AITEMS % NTH == 0) ? t_ + s_ * NTH : min(t_ + s_ * NTH, AITEMS - 1);
+    const int p = item >> 3, c = item & 7;
+    const int gy = ty0 - PH + p / HX, gx = tx0 - PW + p % HX;
+    const int cy = min(max(gy, 0), a.H - 1), cx = min(max(gx, 0), a.W - 1);
+    col = c * 16;
+    return (cy * a.W + cx) * (int)a.xps + (AIN == kInF32 ? 0 : c * 16);
+  };
   unsigned aok = 0u;
 #pragma unroll
   for (int s_ = 0; s_ < APER; ++s_) {
     const int item = (AITEMS % NTH == 0) ? tid + s_ * NTH : min(tid + s_ * NTH, AITEMS - 1);
-    const int p = item >> 3, c = item & 7;
+    const int p = item >> 3;
     const int gy = ty0 - PH + p / HX, gx = tx0 - PW + p % HX;
     const bool ok = static_cast<unsigned>(gy) < static_cast<unsigned>(a.H) && static_cast<unsigned>(gx) < static_cast<unsigned>(a.W);
-    const int cy = min(max(gy, 0), a.H - 1), cx = min(max(gx, 0), a.W - 1);
-    const int off = (cy * a.W + cx) * (int)a.xps + (AIN == kInF32 ? 0 : c * 16);
-    aoff[s_] = off;
-    acol[s_] = c * 16;
     aok |= (ok ? 1u : 0u) << s_;
   }
   int boff[BPER];
@@ -208,10 +214,12 @@ __global__ __launch_bounds__(64 * WM * WN, WM * WN == 8 ? 1 : 2) void conv_s32_k
   for (int s_ = 0; s_ < BPER; ++s_) boff[s_] = (n0 + (tid + s_ * NTH) / 8) * 128 + ((tid + s_ * NTH) & 7) * 16;
 #define OFLOW_LOAD_A(RA, G)                                                                                          \
   _Pragma("unroll") for (int s_ = 0; s_ < APER; ++s_) {                                                              \
+    int col_;                                                                                                        \
+    const int off_ = a_off(s_, col_);                                                                                \
     if constexpr (AIN == kInF32) /* rows of cin floats: channels past cin re-read the row's last 16 B (zeroed) */   \
-      RA[s_] = __builtin_amdgcn_raw_buffer_load_b128(rsA, aoff[s_] + min((G) * 128 + acol[s_], a.cin * 4 - 16), 0, 0); \
+      RA[s_] = __builtin_amdgcn_raw_buffer_load_b128(rsA, off_ + min((G) * 128 + col_, a.cin * 4 - 16), 0, 0);      \
     else                                                                                                             \
-      RA[s_] = __builtin_amdgcn_raw_buffer_load_b128(rsA, aoff[s_], (G) * 128, 0);                                  \
+      RA[s_] = __builtin_amdgcn_raw_buffer_load_b128(rsA, off_, (G) * 128, 0);                                      \
   }
 #define OFLOW_WRITE_A(RA, BUF, G)                                                                                    \
   _Pragma("unroll") for (int s_ = 0; s_ < APER; ++s_) {                                                              \
@@ -464,14 +472,44 @@ __global__ __launch_bounds__(64 * WM * WN, WM * WN == 8 ? 1 : 2) void conv_s32_k
     if (a.y0 == nullptr && a.fn == nullptr) return;
   }
 
-  // S32 / GRU consumers: one thread = one pixel x 8 consecutive channels
+  // S32 / GRU consumers: one thread = one pixel x 8 consecutive channels, KIT items per thread. The GRU state operands
+  // of every item (h; z) are loaded first, all in flight at once, then consumed: one memory round trip per epilogue
+  // instead of one per item.
   constexpr int C8 = BN / 8;
-  for (int item = tid; item < BM * C8; item += NTH) {
+  constexpr int KIT = (BM * C8 + NTH - 1) / NTH;
+  u32x4 pre[EPI == 0 ? 1 : KIT][EPI == 2 ? 4 : 2];
+#pragma unroll
+  for (int k = 0; k < (EPI == 0 ? 0 : KIT); ++k) {
+    const int item = tid + k * NTH;
+    const int pl = item / C8, nl = (item - pl * C8) * 8, n = n0 + nl;
+    const int y = ty0 + pl / kTX, x = tx0 + (pl % kTX);
+    if (item >= BM * C8 || n >= a.N || y >= a.H || x >= a.W) continue;
+    const long long P = pix0 + (long long)y * a.W + x;
+    if constexpr (EPI == 1) {
+      if (n >= a.gch) {
+        const u32x4* hp = reinterpret_cast<const u32x4*>(a.h + P * a.gch + (n - a.gch));
+        pre[k][0] = hp[0];
+        pre[k][1] = hp[1];
+      }
+    } else if constexpr (EPI == 2) {
+      const u32x4* hp = reinterpret_cast<const u32x4*>(a.h + P * a.gch + n);
+      const u32x4* zp = reinterpret_cast<const u32x4*>(a.z + P * a.gch + n);
+      pre[k][0] = hp[0];
+      pre[k][1] = hp[1];
+      pre[k][2] = zp[0];
+      pre[k][3] = zp[1];
+    }
+  }
+  constexpr int UNR = EPI == 0 ? 1 : KIT;  // GRU: unrolled (pre[k] in registers); EPI 0: a plain loop
+#pragma unroll UNR
+  for (int k = 0; k < KIT; ++k) {
+    const int item = tid + k * NTH;
     const int pl = item / C8, c8 = item - pl * C8;
     const int nl = c8 * 8, n = n0 + nl;
     const int y = ty0 + pl / kTX, x = tx0 + (pl % kTX);
-    if (n >= a.N || y >= a.H || x >= a.W) continue;
+    if (item >= BM * C8 || n >= a.N || y >= a.H || x >= a.W) continue;
     const long long P = pix0 + (long long)y * a.W + x;
+    const float* pf = reinterpret_cast<const float*>(&pre[EPI == 0 ? 0 : k][0]);  // GRU: [0..7] h, [8..15] z
     const float4 t0 = *reinterpret_cast<const float4*>(&sT[pl * TS + nl]);
     const float4 t1 = *reinterpret_cast<const float4*>(&sT[pl * TS + nl + 4]);
     float v[8] = {t0.x, t0.y, t0.z, t0.w, t1.x, t1.y, t1.z, t1.w};
@@ -521,22 +559,20 @@ __global__ __launch_bounds__(64 * WM * WN, WM * WN == 8 ? 1 : 2) void conv_s32_k
 #pragma unroll
         for (int j = 0; j < 8; ++j) zp[j] = 1.0f / (1.0f + expf(-v[j]));
       } else {
-        const float* hp = a.h + P * a.gch + (n - a.gch);
         float rh[8];
 #pragma unroll
-        for (int j = 0; j < 8; ++j) rh[j] = (1.0f / (1.0f + expf(-v[j]))) * hp[j];
+        for (int j = 0; j < 8; ++j) rh[j] = (1.0f / (1.0f + expf(-v[j]))) * pf[j];
         store_s32(a.y0, a.y0ps, P, n - a.gch, a.gch, rh);
       }
     } else {
       // candidate + blend (update.py:96-97): h = (1 - z) * h + z * tanh(q); h (fp32) in place + S32 y0
       float* hp = a.h + P * a.gch + n;
-      const float* zp = a.z + P * a.gch + n;
       float hn[8];
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         const float q = tanhf(v[j]);
-        const float z = zp[j];
-        hn[j] = (1.0f - z) * hp[j] + z * q;
+        const float z = pf[8 + j];
+        hn[j] = (1.0f - z) * pf[j] + z * q;
       }
 #pragma unroll
       for (int j = 0; j < 8; ++j) hp[j] = hn[j];
