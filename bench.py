@@ -68,6 +68,43 @@ def pyramid_cost(batch: int, dims, c: int = 256):
     return flops, write + read
 
 
+def lookup_api_leg(ppg: int, dims, flow_low, dev, reps: int = 12):
+    """The reference's lookup operator (CorrBlock.__call__, corr.py:56-77: NCHW fp32 out) on this workload's shapes,
+    timed after the timed region (in the step the lookup runs inside convc1): a (ppg, 256, H/8, W/8) feature pair
+    per pyramid (synthetic features, two pyramids alternating so that no launch finds its pyramid in the 256 MiB
+    Infinity Cache), the step's own final coordinates (grid + its last low-res flow), ``reps`` launches each timed with
+    HIP events on the launch stream. Roofline = SURVEY §8(d)'s algorithmic bytes / mean launch time."""
+    from model import CorrBlock, synthetic
+    from model.utils import coords_grid
+
+    h0, w0 = dims[0]
+    blocks = []
+    for k in range(2):
+        f1, f2 = synthetic.synthetic_fmaps(ppg, 256, h0, w0, stream=40 + k)
+        blocks.append(CorrBlock(f1.to(dev), f2.to(dev)))
+    coords = (coords_grid(ppg, h0, w0).to(dev) + flow_low[:ppg].float()).contiguous()
+    st = torch.cuda.current_stream(dev)
+    ts = []
+    for i in range(reps + 2):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(st)
+        blocks[i % 2](coords)
+        e1.record(st)
+        e1.synchronize()
+        if i >= 2:
+            ts.append(e0.elapsed_time(e1))
+    ms = statistics.fmean(ts)
+    nbytes = lookup_bytes(ppg, dims)
+    ach = nbytes / (ms * 1e-3) / 1e9
+    return {
+        "note": "CorrBlock.__call__ (API form, NCHW fp32, corr_lookup_tiled kernel) on this workload's shapes and final "
+        "coordinates, timed after the timed region; not part of the step (the step's lookup runs inside convc1)",
+        "bound": "hbm", "launch_ms": round(ms, 5), "launches": len(ts), "algorithmic_bytes_per_launch": nbytes,
+        "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4),
+        "traffic": pmc_traffic("sintel" if h0 == 55 else "kitti", ppg, "corr_lookup_api"),
+    }
+
+
 def fused_lookup_bytes(batch: int, dims, lanes: int, radius: int = 4) -> int:
     """Algorithmic HBM bytes of the fused lookup + convc1 per iteration over ``batch`` pairs in ``lanes`` launches:
     per query the lookup's window reads (SURVEY §8(d) term 1) + its coordinates (8 B) + the S32 output (256 channels
@@ -311,6 +348,10 @@ def main() -> int:
         elapsed = time.perf_counter() - t0
         _native.set_event_recorder(None)
 
+    api_lookup = None
+    if rank == 0 and rec is not None and args.workload in ("sintel", "kitti") and not alt:
+        api_lookup = lookup_api_leg(ppg, dims, out[0], dev)
+
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -384,8 +425,11 @@ def main() -> int:
             "mfma": {"executed_f16_tflops": round(tf, 1), "peak_tflops": MFMA_F16_PEAK_TFLOPS,
                      "frac": round(tf / MFMA_F16_PEAK_TFLOPS, 4), "flops_per_launch": flops},
         }
+        line["kernels"] = {}
         if pk:
-            line["kernels"] = {"corr_pyramid": pyramid_entry(pk, ppg, dims)}
+            line["kernels"]["corr_pyramid"] = pyramid_entry(pk, ppg, dims)
+        if api_lookup is not None:
+            line["kernels"]["corr_lookup_api"] = api_lookup
     elif rec and rec.get("corr_lookup"):
         lk = rec.get("corr_lookup", [])
         pk = rec.get("corr_pyramid", [])

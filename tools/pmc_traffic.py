@@ -10,11 +10,13 @@ Corrections (gfx950):
     64-B sectors), so each request is one 128-B line: read bytes = TCC_EA0_RDREQ_sum x 128.
   * writes: WRITE_SIZE (KiB) is exact for this kernel: 71,280 KiB = the 72.99 MB fp32 output, per launch.
 
-usage: python tools/pmc_traffic.py <rdreq_counter_collection.csv> <write_size_counter_collection.csv> <key>
+usage: python tools/pmc_traffic.py <rdreq_counter_collection.csv> <write_size_counter_collection.csv> <key> [kernel regex]
+(key = "<workload>:<pairs per GPU>:<kernel tag>", the name bench.py looks up; the regex selects the kernel's rows)
 """
 import csv
 import json
 import os
+import re
 import statistics
 import sys
 
@@ -22,8 +24,13 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 OUT = os.path.join(REPO, "profiles", "lookup_traffic.json")
 
 
-def per_launch(path, counter):
-    vals = [float(r["Counter_Value"]) for r in csv.DictReader(open(path)) if r["Counter_Name"] == counter]
+def per_launch(path, counter, regex=None):
+    pat = re.compile(regex) if regex else None
+    rows = [r for r in csv.DictReader(open(path))
+            if r["Counter_Name"] == counter and (pat is None or pat.search(r.get("Kernel_Name", "")))]
+    # the bench's own launches are the largest grid (the golden-EPE check before the timed region runs 1 pair)
+    big = max((int(r["Grid_Size"]) for r in rows), default=0)
+    vals = [float(r["Counter_Value"]) for r in rows if int(r["Grid_Size"]) == big]
     if not vals:
         raise SystemExit(f"{path}: no {counter} rows")
     return statistics.median(vals), len(vals)
@@ -31,8 +38,9 @@ def per_launch(path, counter):
 
 def main():
     rd_csv, wr_csv, key = sys.argv[1:4]
-    req, n1 = per_launch(rd_csv, "TCC_EA0_RDREQ_sum")
-    wr_kib, n2 = per_launch(wr_csv, "WRITE_SIZE")
+    regex = sys.argv[4] if len(sys.argv) > 4 else None
+    req, n1 = per_launch(rd_csv, "TCC_EA0_RDREQ_sum", regex)
+    wr_kib, n2 = per_launch(wr_csv, "WRITE_SIZE", regex)
     rd, wr = int(req * 128), int(wr_kib * 1024)
     data = json.load(open(OUT)) if os.path.exists(OUT) else {}
     data[key] = {

@@ -5,7 +5,7 @@ A step is anchored on the corr-pyramid launch (one per RAFT forward): the span f
 anchor holds exactly one step's kernels. The last `--steps` anchors are used (the timed region), giving
 steps - 1 full spans. Prints ms/step, share, launches/step and mean duration per kernel, plus span / busy / idle.
 
-usage: python tools/prof_summary.py <run_results.db | kernel_trace.csv> [--steps 5] [--anchor corr_pyramid]
+usage: python tools/prof_summary.py <run_results.db | kernel_trace.csv> [--steps 5] [--anchor corr_pyramid] [--skip-last 2]
 """
 import argparse
 import collections
@@ -36,6 +36,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("path")
     ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--skip-last", type=int, default=0,
+                    help="anchors after the timed region to ignore (bench.py's API lookup leg builds 2 pyramids)")
     ap.add_argument("--anchor", default="corr_pyramid")
     ap.add_argument("--top", type=int, default=40)
     a = ap.parse_args()
@@ -43,7 +45,7 @@ def main():
     anchors = [i for i, r in enumerate(rows) if a.anchor in r[0]]
     if len(anchors) < 2:
         raise SystemExit(f"need >= 2 '{a.anchor}' launches, found {len(anchors)}")
-    sel = anchors[-a.steps:]
+    sel = anchors[: len(anchors) - a.skip_last][-a.steps:]
     lo, hi = sel[0], sel[-1]
     spans = len(sel) - 1
     part = rows[lo:hi]

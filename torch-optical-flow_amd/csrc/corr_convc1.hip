@@ -2,23 +2,24 @@
 //
 // Replaces, in the RAFT forward, `corr = corr_fn(coords1)` (methods/raft/model/raft.py:128 -> corr.py:56-77) followed
 // by `F.relu(self.convc1(corr))` (update.py:120-121, a 1x1 conv L*(2r+1)^2 -> 256): the (B, 324, H, W) lookup volume
-// never reaches HBM. Per workgroup of 128 query pixels, level by level:
+// never reaches HBM. Per workgroup of 64 query pixels (4 waves; two workgroups per CU, so one's gather / tap phases
+// overlap the other's MFMAs), level by level:
 //   1. the (2r+2)^2 window patches of the level, gathered from the tiled pyramid (4x8 tiles = 128-B lines, the
-//      layout corr_lookup.hip reads; 25 scalar loads per thread, issued one level ahead so that they fly during the
-//      previous level's MFMAs), are written to LDS (odd per-query stride);
+//      layout corr_lookup.hip reads; 25 scalar loads per thread, issued during the previous level's last MFMAs), are
+//      written to LDS (odd per-query stride);
 //   2. the (2r+1)^2 bilinear taps of each query (bilinear4: the lookup kernels' arithmetic, bit for bit) become the
 //      level's split-fp16 A operand in LDS: [k32 group][pixel][hi 32 | lo 32], 16-B slots XOR-swizzled, one thread per
 //      (pixel, 8-tap slot) writing whole 16-B slots; taps past (2r+1)^2 in the level's last group stay zero;
-//   3. 8 waves (2 pixel halves x 4 channel quarters, 64 x 64 each) run the level's G k32 groups as split-fp16 products
-//      on v_mfma_f32_32x32x16_f16 (hi*lo + lo*hi + hi*hi, fp32 accumulate: conv_s32.hip's arithmetic); the weights
-//      stream one k32 group (256 channels x 128 B) at a time through a double buffer over the dead patches, each group
-//      register-staged one group ahead (the next level's first group behind the level's last MFMAs).
+//   3. each wave (64 pixels x 64 output channels) runs the level's G k32 groups as split-fp16 products on
+//      v_mfma_f32_32x32x16_f16 (hi*lo + lo*hi + hi*hi, fp32 accumulate: conv_s32.hip's arithmetic); the weights
+//      stream one k32 group (256 channels x 128 B) at a time through LDS over the dead patches, register-staged one
+//      group ahead.
 // Epilogue: accumulators -> LDS [pixel][channel] fp32 -> per-channel weight scale, bias, ReLU -> S32 store of the 256
 // output channels (convc2's input).
 //
 // Weights: oflow_conv_s32's packing of convc1 with its input channels regrouped per level: level l's tap k at packed
-// channel l*G*32 + k (G = ceil((2r+1)^2 / 32)); the other channels are zero. Radius 3 (G = 2) and 4 (G = 3), <= 4 levels.
-// LDS: A G*16 KB + weights/patches 64 KB + epilogue tile overlay = 130 KB (one workgroup of 8 waves per CU, 226 VGPRs).
+// channel l*G*32 + k (G = ceil((2r+1)^2 / 32)); the other channels are zero. Radius 3 (G = 2) and 4 (G = 3).
+// LDS: A G*8 KB + weights/patches 32 KB, epilogue tile overlay 66.5 KB, + 5.5 KB (two workgroups per CU).
 #include "oflow_internal.h"
 
 namespace oflow {
@@ -28,8 +29,8 @@ typedef _Float16 half8 __attribute__((ext_vector_type(8)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 
-constexpr int kQM = 128;  // query pixels per workgroup
-constexpr int kNT = 512;  // threads: 8 waves = 2 (pixel halves) x 4 (channel quarters)
+constexpr int kQM = 64;   // query pixels per workgroup
+constexpr int kNT = 256;  // threads: 4 waves, one per 64-channel quarter (64 pixels x 64 channels each)
 constexpr int kN = 256;   // convc1 output channels (update.py:114)
 
 __device__ __forceinline__ int swz(int row) { return (row >> 1) & 7; }
@@ -52,12 +53,12 @@ struct C1Args {
 };
 
 template <int R>
-__global__ __launch_bounds__(kNT, 1) void corr_convc1_kernel(C1Args a) {
+__global__ __launch_bounds__(kNT, 2) void corr_convc1_kernel(C1Args a) {
   constexpr int PK = 2 * R + 2, K = 2 * R + 1, KK = K * K, PS = PK * PK, QS = PS + 1;
   constexpr int G = (KK + 31) / 32;      // k32 groups per level
   constexpr int NSLOT = (KK + 7) / 8;    // 8-tap slots that hold taps
   constexpr int A_BYTES = G * kQM * 128;
-  constexpr int B_BYTES = 2 * kN * 128;  // two k32 weight groups (double buffer)
+  constexpr int B_BYTES = kN * 128;      // one k32 weight group
   constexpr int P_BYTES = kQM * QS * 4;
   constexpr int TS = kN + 4;             // epilogue tile row (floats)
   constexpr int EPI_BYTES = kQM * TS * 4;
@@ -77,7 +78,7 @@ __global__ __launch_bounds__(kNT, 1) void corr_convc1_kernel(C1Args a) {
   float* sP = reinterpret_cast<float*>(sB);
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wm = wave >> 2, wn = wave & 3;
+  const int wn = wave;
   const int r = lane & 31, hh = lane >> 5;
   const int q0 = blockIdx.x * kQM;
   const int nq = min(kQM, a.total - q0);
@@ -152,11 +153,11 @@ __global__ __launch_bounds__(kNT, 1) void corr_convc1_kernel(C1Args a) {
 #pragma unroll
     for (int s = 0; s < BI; ++s) rb[s] = *reinterpret_cast<const u32x4*>(wg + (size_t)(tid + kNT * s) * 16);
   };
-  auto write_w = [&](int buf) {
+  auto write_w = [&]() {
 #pragma unroll
     for (int s = 0; s < BI; ++s) {
       const int c = tid + kNT * s, n = c >> 3, sl = c & 7;
-      *reinterpret_cast<u32x4*>(sB + buf * (kN * 128) + n * 128 + ((sl ^ swz(n)) << 4)) = rb[s];
+      *reinterpret_cast<u32x4*>(sB + n * 128 + ((sl ^ swz(n)) << 4)) = rb[s];
     }
   };
 
@@ -168,8 +169,8 @@ __global__ __launch_bounds__(kNT, 1) void corr_convc1_kernel(C1Args a) {
 #pragma unroll
       for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
 
-  gather(0);
   load_w(0, 0);
+  gather(0);
   for (int l = 0; l < a.nlev; ++l) {
     // ---- 1. patches -> LDS (over the weight buffer: the previous level's MFMAs are done) ----
 #pragma unroll
@@ -183,7 +184,7 @@ __global__ __launch_bounds__(kNT, 1) void corr_convc1_kernel(C1Args a) {
     __syncthreads();
     // ---- 2. bilinear taps -> split-fp16 A operand: thread = (pixel q, slots S = set, set + 4, ...) ----
     {
-      const int q = tid & (kQM - 1), set = tid >> 7;  // set is uniform per wave
+      const int q = tid & (kQM - 1), set = tid / kQM;  // set (= wave) is uniform per wave
       const float4 w4 = sW[l & 1][q];
       const float* p = sP + q * QS;
 #pragma unroll
@@ -209,36 +210,41 @@ __global__ __launch_bounds__(kNT, 1) void corr_convc1_kernel(C1Args a) {
       }
     }
     if (l + 1 < a.nlev) decode(l + 1);
-    __syncthreads();  // patches dead, A complete, the next level's windows decoded
-    // ---- 3. the level's first weight group -> LDS; the next level's gathers fly during this level's MFMAs ----
-    write_w(0);
-    load_w(l, G > 1 ? 1 : 0);
-    if (l + 1 < a.nlev) gather(l + 1);
-    __syncthreads();
-    half8 ah[2][2], al[2][2], bh[2][2], bl[2][2];  // [buffer][tile]
-    auto read_ops = [&](int buf, int g, int sub) {
+    __syncthreads();  // patches dead (the weight buffer is free), A complete, the next level's windows decoded
+    // ---- 3. the level's k32 groups: weights (held in rb since the previous group) -> LDS, the next group's (or the
+    // next level's first) weights loaded, then the group's MFMAs. The next level's gathers are issued after the
+    // level's last weight load (vmcnt retires in order: a weight wait never waits for them) and fly during the last
+    // group's MFMAs; the other workgroup on the CU covers what they do not hide. ----
+    half8 ah[2][2], al[2][2], bh[2][2], bl[2][2];  // [sub-step][tile]
+    auto read_ops = [&](int g, int sub) {
       const int chi = 2 * sub + hh, clo = 4 + 2 * sub + hh;
 #pragma unroll
       for (int mt = 0; mt < 2; ++mt) {
-        const int pr = wm * 64 + mt * 32 + r;
+        const int pr = mt * 32 + r;
         const uint8_t* row = sA + g * (kQM * 128) + pr * 128;
-        ah[buf][mt] = *reinterpret_cast<const half8*>(row + ((chi ^ swz(pr)) << 4));
-        al[buf][mt] = *reinterpret_cast<const half8*>(row + ((clo ^ swz(pr)) << 4));
+        ah[sub][mt] = *reinterpret_cast<const half8*>(row + ((chi ^ swz(pr)) << 4));
+        al[sub][mt] = *reinterpret_cast<const half8*>(row + ((clo ^ swz(pr)) << 4));
       }
 #pragma unroll
       for (int nt = 0; nt < 2; ++nt) {
         const int n = wn * 64 + nt * 32 + r;
-        const uint8_t* row = sB + (g & 1) * (kN * 128) + n * 128;
-        bh[buf][nt] = *reinterpret_cast<const half8*>(row + ((chi ^ swz(n)) << 4));
-        bl[buf][nt] = *reinterpret_cast<const half8*>(row + ((clo ^ swz(n)) << 4));
+        const uint8_t* row = sB + n * 128;
+        bh[sub][nt] = *reinterpret_cast<const half8*>(row + ((chi ^ swz(n)) << 4));
+        bl[sub][nt] = *reinterpret_cast<const half8*>(row + ((clo ^ swz(n)) << 4));
       }
     };
-    // group g from weight buffer g & 1; behind its MFMAs group g + 1 (held in rb) is written to the other buffer and rb
-    // reloaded with the next group (the next level's first at the last group)
 #pragma unroll
     for (int g = 0; g < G; ++g) {
-      read_ops(0, g, 0);
-      read_ops(1, g, 1);
+      write_w();
+      if (g + 1 < G) {
+        load_w(l, g + 1);
+      } else if (l + 1 < a.nlev) {
+        load_w(l + 1, 0);
+        gather(l + 1);
+      }
+      __syncthreads();  // group g's weights visible
+      read_ops(g, 0);
+      read_ops(g, 1);
 #pragma unroll
       for (int sub = 0; sub < 2; ++sub)
 #pragma unroll
@@ -249,15 +255,8 @@ __global__ __launch_bounds__(kNT, 1) void corr_convc1_kernel(C1Args a) {
             acc[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[sub][mt], bh[sub][nt], acc[mt][nt], 0, 0, 0);
             acc[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[sub][mt], bh[sub][nt], acc[mt][nt], 0, 0, 0);
           }
-      if (g + 1 < G) {
-        write_w((g + 1) & 1);
-        if (g + 2 < G)
-          load_w(l, g + 2);
-        else if (l + 1 < a.nlev)
-          load_w(l + 1, 0);
-      }
-      __syncthreads();  // group g's operand reads done (its buffer is rewritten next); at the last group: before the
-                        // next level's patches / A overwrite the buffers
+      __syncthreads();  // group g's operand reads done: the weight buffer (and at the level's end the patch / A
+                        // buffers) may be overwritten
     }
   }
 
@@ -268,7 +267,7 @@ __global__ __launch_bounds__(kNT, 1) void corr_convc1_kernel(C1Args a) {
 #pragma unroll
     for (int nt = 0; nt < 2; ++nt) {
       const int n = wn * 64 + nt * 32 + r;
-      const int pbase = wm * 64 + mt * 32;
+      const int pbase = mt * 32;
 #pragma unroll
       for (int e = 0; e < 16; ++e) sT[(pbase + (e & 3) + 8 * (e >> 2) + 4 * hh) * TS + n] = acc[mt][nt][e];
     }

@@ -204,7 +204,8 @@ __global__ __launch_bounds__(256) void grid_warp_kernel(WarpArgs a) {
 // budget take the direct-gather loop for that tile). Same arithmetic as grid_warp_kernel: bit-identical results.
 constexpr int kWThreads = 256, kWWaves = kWThreads / 64;
 constexpr int kWTY = 16, kWTX = 64, kWRows = kWTY / kWWaves;
-constexpr int kBoxFloats = 12288;  // 48 KB: a 16 x 64 tile with a +-32 px margin fits
+constexpr int kBoxFloats = 9216;  // 36 KB (4 workgroups per CU): a 16 x 64 tile with a +-27 px margin (N(0, 8^2) px flow) fits
+constexpr int kWChunks = kBoxFloats / 4 / kWThreads;  // 16-B box chunks per thread (12)
 
 template <bool FLOW>
 __global__ __launch_bounds__(kWThreads) void warp_bilinear_lds_kernel(WarpArgs a, int tiles_x, int tiles_y) {
@@ -330,40 +331,40 @@ __global__ __launch_bounds__(kWThreads) void warp_bilinear_lds_kernel(WarpArgs a
     }
     return;
   }
-  for (int c = 0; c < a.C; ++c) {
-    const float* __restrict__ sc = src + (size_t)c * HW;
-    {
-      if (c) __syncthreads();  // every thread is done reading channel c-1's box
-      // flat index over 16-B chunks of the box rows (i = tid + kWThreads j -> (row, chunk), stepped incrementally);
-      // 8 chunks in flight per thread; the box starts on a 4-float boundary and rows are 16-B aligned
-      const int cw = bw >> 2, n = cw * bh, dr = kWThreads / cw, dc = kWThreads - dr * cw;
-      const float* base = sc + (size_t)ymin * a.W + xmin;
-      int r = tid / cw, col = tid - r * cw;
-      for (int i0 = tid; i0 < n; i0 += 8 * kWThreads) {
-        float4 v[8];
-        int off[8];
+  // Channel pipeline: the box of channel c + 1 is loaded into registers (16-B chunks, kWChunks per thread, all in
+  // flight) while channel c is interpolated from LDS, then written over it: one L2 round trip per channel is hidden
+  // behind the previous channel's taps instead of serialised with them.
+  const int cw = bw >> 2, n = cw * bh, dr = kWThreads / cw, dc = kWThreads - dr * cw;
+  float4 stage[kWChunks];
+  // chunk j of this thread -> (box row, 16-B column), stepped incrementally from tid
+  auto chunk_walk = [&](auto&& fn) {
+    int r = tid / cw, col = tid - r * cw;
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          off[j] = r * bw + col * 4;
-          if (i0 + kWThreads * j < n) {
-            const int x = xmin + col * 4;
-            const float* q = base + (size_t)r * a.W + col * 4;
-            v[j] = x + 3 < a.W ? *reinterpret_cast<const float4*>(q)  // never read past the row's end
-                               : make_float4(q[0], x + 1 < a.W ? q[1] : 0.f, x + 2 < a.W ? q[2] : 0.f, 0.f);
-          }
-          r += dr;
-          col += dc;
-          if (col >= cw) {
-            col -= cw;
-            ++r;
-          }
-        }
-#pragma unroll
-        for (int j = 0; j < 8; ++j)
-          if (i0 + kWThreads * j < n) *reinterpret_cast<float4*>(&sBox[off[j]]) = v[j];
+    for (int j = 0; j < kWChunks; ++j) {
+      if (tid + kWThreads * j < n) fn(j, r, col);
+      r += dr;
+      col += dc;
+      if (col >= cw) {
+        col -= cw;
+        ++r;
       }
-      __syncthreads();
     }
+  };
+  auto load_box = [&](int c) {
+    const float* base = src + (size_t)c * HW + (size_t)ymin * a.W + xmin;
+    chunk_walk([&](int j, int r, int col) {
+      const int x = xmin + col * 4;
+      const float* q = base + (size_t)r * a.W + col * 4;
+      stage[j] = x + 3 < a.W ? *reinterpret_cast<const float4*>(q)  // never read past the row's end
+                             : make_float4(q[0], x + 1 < a.W ? q[1] : 0.f, x + 2 < a.W ? q[2] : 0.f, 0.f);
+    });
+  };
+  load_box(0);
+  for (int c = 0; c < a.C; ++c) {
+    if (c) __syncthreads();  // every thread is done reading channel c-1's box
+    chunk_walk([&](int j, int r, int col) { *reinterpret_cast<float4*>(&sBox[r * bw + col * 4]) = stage[j]; });
+    __syncthreads();
+    if (c + 1 < a.C) load_box(c + 1);
 #pragma unroll
     for (int k = 0; k < kWRows; ++k) {
       if (!((vmask >> (16 + k)) & 1u)) continue;
