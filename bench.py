@@ -132,19 +132,24 @@ def pmc_traffic(workload: str, ppg: int, kernel: str):
     return tr.get("hbm_bytes_per_launch") if tr else None
 
 
-def pyramid_entry(pk, ppg: int, dims):
+def pyramid_entry(pk, ppg: int, dims, split: bool = False):
+    """The corr pyramid kernel's rate. split: the RAFT forward's split-fp16 build (oflow_corr_pyramid_tiled_s32: three
+    f16 MFMAs per product, so executed f16 flops = 3x the GEMM's, against the dense f16 peak); else fp32 MFMA."""
     pk_ms = mean_ms(pk)
     flops, nbytes = pyramid_cost(ppg, dims)
-    tf = flops / (pk_ms * 1e-3) / 1e12
+    exe = 3 * flops if split else flops
+    peak = MFMA_F16_PEAK_TFLOPS if split else MFMA_F32_PEAK_TFLOPS
+    tf = exe / (pk_ms * 1e-3) / 1e12
     return {
         "bound": "mfma",
-        "note": "in-step: runs beside cnet (side stream); alone: tools/kbench.py",
+        "kernel": "corr_pyramid_s32 (split-fp16 products)" if split else "corr_pyramid (fp32 MFMA)",
+        "note": "in-step: runs after fnet; alone: tools/kbench.py",
         "launch_ms": round(pk_ms, 4),
         "achieved_tflops": round(tf, 2),
-        "peak_tflops": MFMA_F32_PEAK_TFLOPS,
-        "frac": round(tf / MFMA_F32_PEAK_TFLOPS, 4),
+        "peak_tflops": peak,
+        "frac": round(tf / peak, 4),
         "hbm_gbs": round(nbytes / (pk_ms * 1e-3) / 1e9, 1),
-        "flops_per_launch": flops,
+        "flops_per_launch": exe,
         "bytes_per_launch": nbytes,
     }
 
@@ -348,6 +353,9 @@ def main() -> int:
         elapsed = time.perf_counter() - t0
         _native.set_event_recorder(None)
 
+    # the RAFT forward builds its pyramid from split-fp16 features (split encoders + CorrBlock); the "corr" workload
+    # calls the CorrBlock API (fp32 MFMA pyramid)
+    split_pyr = model.split_corr and args.update_impl == "split" and args.workload != "corr" and not alt
     api_lookup = None
     if rank == 0 and rec is not None and args.workload in ("sintel", "kitti") and not alt:
         api_lookup = lookup_api_leg(ppg, dims, out[0], dev)
@@ -373,8 +381,12 @@ def main() -> int:
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": ("fp16 features, fp32 accumulate (on-the-fly corr); " if alt else "fp32 corr (fp32 MFMA); ")
-        + ("convs split-fp16 (22-bit operands: fp16 hi + lo, 3 MFMA per product, fp32 accumulate)"
+        "dtype": ("fp16 features, fp32 accumulate (on-the-fly corr); " if alt
+                  else "corr + convs split-fp16 (22-bit operands: fp16 hi + lo, 3 f16 MFMA per product, fp32 accumulate); "
+                  "lookup fp32" if split_pyr
+                  else "fp32 corr (fp32 MFMA); ")
+        + ("" if split_pyr
+           else "convs split-fp16 (22-bit operands: fp16 hi + lo, 3 MFMA per product, fp32 accumulate)"
            if args.update_impl == "split" else "update convs fp32 (MIOpen)"),
         "data": "synthetic (integer texture frames with a known (3, -1.5) px shift; hash-initialised weights)",
         "config": {
@@ -427,7 +439,7 @@ def main() -> int:
         }
         line["kernels"] = {}
         if pk:
-            line["kernels"]["corr_pyramid"] = pyramid_entry(pk, ppg, dims)
+            line["kernels"]["corr_pyramid"] = pyramid_entry(pk, ppg, dims, split=split_pyr)
         if api_lookup is not None:
             line["kernels"]["corr_lookup_api"] = api_lookup
     elif rec and rec.get("corr_lookup"):
@@ -452,7 +464,7 @@ def main() -> int:
             "launches": len(lk),
         }
         if pk:
-            line["kernels"] = {"corr_pyramid": pyramid_entry(pk, ppg, dims)}
+            line["kernels"] = {"corr_pyramid": pyramid_entry(pk, ppg, dims, split=split_pyr)}
     if epe is not None:
         line["epe_vs_reference"] = {k: (round(v, 8) if isinstance(v, float) else v) for k, v in epe.items()}
     if rank == 0 and world == 1 and not args.no_cpu_baseline and args.workload in ("sintel", "kitti"):

@@ -98,6 +98,12 @@ int oflow_corr_lookup_f32(const float* const* d_levels, const int* level_h, cons
 long long oflow_corr_tiled_level_floats(int H_l, int W_l);
 int oflow_corr_pyramid_tiled_f32(const float* d_fmap1, const float* d_fmap2, int B, int C, int H, int W,
                                  int num_levels, float* const* d_levels, void* stream);
+/* oflow_corr_pyramid_tiled_s32: oflow_corr_pyramid_tiled_f32's levels (same tiled layout) from feature maps given as
+ * S32 rows (B, H, W, C/32 groups of hi[32] | lo[32] fp16; C % 32 == 0; 16-B aligned) -- the RAFT forward's pyramid,
+ * fed by the feature encoder's last convolution: products as three fp16 MFMAs on the hi/lo split (22-bit operands,
+ * fp32 accumulation), not fp32 MFMAs. Within SURVEY §8(c)'s pyramid tolerance of the fp32 result (tested). */
+int oflow_corr_pyramid_tiled_s32(const void* d_fmap1_s32, const void* d_fmap2_s32, int B, int C, int H, int W,
+                                 int num_levels, float* const* d_levels, void* stream);
 int oflow_corr_lookup_tiled_f32(const float* const* d_levels, const int* level_h, const int* level_w,
                                 int num_levels, const float* d_coords, int B, int H, int W, int radius,
                                 float* d_out, void* stream);

@@ -123,50 +123,12 @@ __device__ __forceinline__ size_t lvl_off(const PyramidArgs& p, int l, size_t q,
   }
 }
 
-template <bool VEC, bool TILED>
-__global__ __launch_bounds__(kThreads, 2) void corr_pyramid_kernel(PyramidArgs p) {
-  __shared__ __attribute__((aligned(16))) float sA[2][kBK][kBM];
-  __shared__ __attribute__((aligned(16))) float sB[2][kBK][kBN];
-
+// Epilogue shared by the fp32 and split-fp16 kernels (both leave the same 32x32 C/D accumulator map): scale by 1/sqrt(C),
+// level-0 store, levels 1..3 pooled in registers.
+template <bool TILED>
+__device__ __forceinline__ void pyramid_epilogue(const PyramidArgs& p, f32x16 (&acc)[kTR], int i0, int ty0, int tx0, int b) {
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
-  const int tile = blockIdx.x;
-  const int ty0 = (tile / p.tiles_x) * kTR;
-  const int tx0 = (tile % p.tiles_x) * kTC;
-  const int i0 = blockIdx.y * kBM;
-  const int b = blockIdx.z;
-  const float* F1 = p.f1 + (size_t)b * p.C * p.N;
-  const float* F2 = p.f2 + (size_t)b * p.C * p.N;
-
-  f32x16 acc[kTR];
-#pragma unroll
-  for (int n = 0; n < kTR; ++n) acc[n] = f32x16{0};
-
-  Stage<VEC> st;
-  const int nk = (p.C + kBK - 1) / kBK;
-  st.load(p, F1, F2, 0, i0, ty0, tx0);
-  st.store(sA[0], sB[0]);
-  __syncthreads();
-
-  const int kl = lane >> 5;          // k within an MFMA k-step (32x32x2: lanes 32-63 hold k = 1)
-  const int ml = wave * 32 + (lane & 31);
-  const int nl = lane & 31;
-  for (int c = 0; c < nk; ++c) {
-    const int buf = c & 1;
-    if (c + 1 < nk) st.load(p, F1, F2, (c + 1) * kBK, i0, ty0, tx0);
-#pragma unroll
-    for (int kk = 0; kk < kBK; kk += 2) {
-      const float av = sA[buf][kk + kl][ml];
-#pragma unroll
-      for (int n = 0; n < kTR; ++n) {
-        const float bv = sB[buf][kk + kl][n * kTC + nl];
-        acc[n] = __builtin_amdgcn_mfma_f32_32x32x2f32(av, bv, acc[n], 0, 0, 0);
-      }
-    }
-    if (c + 1 < nk) st.store(sA[buf ^ 1], sB[buf ^ 1]);
-    __syncthreads();
-  }
-
   // ---- epilogue: scale, level-0 store, in-register pooled levels 1..3 ----
   const int tx = lane & 31;
   const int qbase = i0 + wave * 32 + 4 * (lane >> 5);
@@ -242,6 +204,152 @@ __global__ __launch_bounds__(kThreads, 2) void corr_pyramid_kernel(PyramidArgs p
       if (ok && i < p.N) p.lv[3][lvl_off<TILED>(p, 3, (size_t)b * Nn + i, y3, x3)] = v3;
     }
   }
+}
+
+template <bool VEC, bool TILED>
+__global__ __launch_bounds__(kThreads, 2) void corr_pyramid_kernel(PyramidArgs p) {
+  __shared__ __attribute__((aligned(16))) float sA[2][kBK][kBM];
+  __shared__ __attribute__((aligned(16))) float sB[2][kBK][kBN];
+
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int tile = blockIdx.x;
+  const int ty0 = (tile / p.tiles_x) * kTR;
+  const int tx0 = (tile % p.tiles_x) * kTC;
+  const int i0 = blockIdx.y * kBM;
+  const int b = blockIdx.z;
+  const float* F1 = p.f1 + (size_t)b * p.C * p.N;
+  const float* F2 = p.f2 + (size_t)b * p.C * p.N;
+
+  f32x16 acc[kTR];
+#pragma unroll
+  for (int n = 0; n < kTR; ++n) acc[n] = f32x16{0};
+
+  Stage<VEC> st;
+  const int nk = (p.C + kBK - 1) / kBK;
+  st.load(p, F1, F2, 0, i0, ty0, tx0);
+  st.store(sA[0], sB[0]);
+  __syncthreads();
+
+  const int kl = lane >> 5;          // k within an MFMA k-step (32x32x2: lanes 32-63 hold k = 1)
+  const int ml = wave * 32 + (lane & 31);
+  const int nl = lane & 31;
+  for (int c = 0; c < nk; ++c) {
+    const int buf = c & 1;
+    if (c + 1 < nk) st.load(p, F1, F2, (c + 1) * kBK, i0, ty0, tx0);
+#pragma unroll
+    for (int kk = 0; kk < kBK; kk += 2) {
+      const float av = sA[buf][kk + kl][ml];
+#pragma unroll
+      for (int n = 0; n < kTR; ++n) {
+        const float bv = sB[buf][kk + kl][n * kTC + nl];
+        acc[n] = __builtin_amdgcn_mfma_f32_32x32x2f32(av, bv, acc[n], 0, 0, 0);
+      }
+    }
+    if (c + 1 < nk) st.store(sA[buf ^ 1], sB[buf ^ 1]);
+    __syncthreads();
+  }
+
+  pyramid_epilogue<TILED>(p, acc, i0, ty0, tx0, b);
+}
+
+// ---------------------------------------------------------------------------------------------------------------
+// Split-fp16 variant (the RAFT forward's pyramid): both feature maps come as S32 rows (include/oflow.h: per pixel
+// C/32 groups of hi[32] | lo[32] fp16, written directly by the feature encoder's last convolution), and every product
+// is three v_mfma_f32_32x32x16_f16 (hi*lo + lo*hi + hi*hi, fp32 accumulate; conv_s32.hip's arithmetic: 22-bit operands,
+// the lo*lo term below fp32 rounding) instead of fp32 MFMAs at 1/16 of the f16 rate. Same workgroup tile, wave map and
+// 32x32 C/D accumulator map as corr_pyramid_kernel, so the fused pooling epilogue is the same code.
+// Per k32 group: A = 128 query rows x 128 B, B = 256 target rows x 128 B staged in LDS (16-B slots XOR-swizzled as in
+// conv_s32.hip: conflict-free ds_read_b128), the next group register-staged behind the MFMAs; rows outside the image
+// load a clamped pixel and stage as zeros.
+__device__ __forceinline__ int swz8(int row) { return (row >> 1) & 7; }
+
+template <bool TILED>
+__global__ __launch_bounds__(kThreads, 2) void corr_pyramid_s32_kernel(PyramidArgs p, const uint8_t* F1s, const uint8_t* F2s) {
+  typedef _Float16 half8 __attribute__((ext_vector_type(8)));
+  typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+  constexpr int AP = kBM * 8 / kThreads;  // 16-B chunks per thread: A 4, B 8
+  constexpr int BP = kBN * 8 / kThreads;
+  __shared__ __attribute__((aligned(16))) uint8_t sA[kBM * 128];
+  __shared__ __attribute__((aligned(16))) uint8_t sB[kBN * 128];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tile = blockIdx.x;
+  const int ty0 = (tile / p.tiles_x) * kTR;
+  const int tx0 = (tile % p.tiles_x) * kTC;
+  const int i0 = blockIdx.y * kBM;
+  const int b = blockIdx.z;
+  const int G = p.C >> 5;
+  const int ps = G * 128;  // bytes per pixel row
+  const uint8_t* A0 = F1s + (size_t)b * p.N * ps;
+  const uint8_t* B0 = F2s + (size_t)b * p.N * ps;
+
+  int aoff[AP], boff[BP];
+  unsigned okm = 0u;
+#pragma unroll
+  for (int s = 0; s < AP; ++s) {
+    const int c = tid + kThreads * s, row = c >> 3, sl = c & 7;
+    const int i = i0 + row;
+    okm |= (i < p.N ? 1u : 0u) << s;
+    aoff[s] = min(i, p.N - 1) * ps + sl * 16;
+  }
+#pragma unroll
+  for (int s = 0; s < BP; ++s) {
+    const int c = tid + kThreads * s, row = c >> 3, sl = c & 7;
+    const int y = ty0 + (row >> 5), x = tx0 + (row & 31);
+    const bool ok = y < p.H && x < p.W;
+    okm |= (ok ? 1u : 0u) << (AP + s);
+    boff[s] = (min(y, p.H - 1) * p.W + min(x, p.W - 1)) * ps + sl * 16;
+  }
+  u32x4 ra[AP], rb[BP];
+  auto load = [&](int g) {
+#pragma unroll
+    for (int s = 0; s < AP; ++s) ra[s] = *reinterpret_cast<const u32x4*>(A0 + aoff[s] + g * 128);
+#pragma unroll
+    for (int s = 0; s < BP; ++s) rb[s] = *reinterpret_cast<const u32x4*>(B0 + boff[s] + g * 128);
+  };
+  auto write = [&]() {
+    const u32x4 z = {0u, 0u, 0u, 0u};
+#pragma unroll
+    for (int s = 0; s < AP; ++s) {
+      const int c = tid + kThreads * s, row = c >> 3, sl = c & 7;
+      *reinterpret_cast<u32x4*>(sA + row * 128 + ((sl ^ swz8(row)) << 4)) = ((okm >> s) & 1u) ? ra[s] : z;
+    }
+#pragma unroll
+    for (int s = 0; s < BP; ++s) {
+      const int c = tid + kThreads * s, row = c >> 3, sl = c & 7;
+      *reinterpret_cast<u32x4*>(sB + row * 128 + ((sl ^ swz8(row)) << 4)) = ((okm >> (AP + s)) & 1u) ? rb[s] : z;
+    }
+  };
+
+  f32x16 acc[kTR];
+#pragma unroll
+  for (int n = 0; n < kTR; ++n) acc[n] = f32x16{0};
+  const int r = lane & 31, hh = lane >> 5;
+  const int arow = wave * 32 + r;
+  load(0);
+  for (int g = 0; g < G; ++g) {
+    if (g) __syncthreads();  // every wave is done reading group g-1
+    write();
+    __syncthreads();
+    if (g + 1 < G) load(g + 1);
+#pragma unroll
+    for (int sub = 0; sub < 2; ++sub) {
+      const int chi = 2 * sub + hh, clo = 4 + 2 * sub + hh;
+      const half8 ah = *reinterpret_cast<const half8*>(sA + arow * 128 + ((chi ^ swz8(arow)) << 4));
+      const half8 al = *reinterpret_cast<const half8*>(sA + arow * 128 + ((clo ^ swz8(arow)) << 4));
+#pragma unroll
+      for (int n = 0; n < kTR; ++n) {
+        const int brow = n * kTC + r;
+        const half8 bh = *reinterpret_cast<const half8*>(sB + brow * 128 + ((chi ^ swz8(brow)) << 4));
+        const half8 bl = *reinterpret_cast<const half8*>(sB + brow * 128 + ((clo ^ swz8(brow)) << 4));
+        acc[n] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bl, acc[n], 0, 0, 0);
+        acc[n] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, bh, acc[n], 0, 0, 0);
+        acc[n] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bh, acc[n], 0, 0, 0);
+      }
+    }
+  }
+  pyramid_epilogue<TILED>(p, acc, i0, ty0, tx0, b);
 }
 
 // Levels >= 4 (num_levels > 4 only): plain floor 2x2 average pool of the level above.
@@ -377,6 +485,56 @@ static int corr_pyramid_impl(const float* d_fmap1, const float* d_fmap2, int B, 
     else
       hipLaunchKernelGGL(avgpool2x2_kernel, dim3(blocks), dim3(256), 0, s, d_levels[l - 1], d_levels[l], planes,
                          hl[l - 1], wl[l - 1], hl[l], wl[l]);
+    st = launch_status();
+    if (st != OFLOW_OK) return st;
+  }
+  return OFLOW_OK;
+}
+
+extern "C" int oflow_corr_pyramid_tiled_s32(const void* d_fmap1_s32, const void* d_fmap2_s32, int B, int C, int H, int W,
+                                            int num_levels, float* const* d_levels, void* stream) {
+  if (!d_fmap1_s32 || !d_fmap2_s32 || !d_levels) return OFLOW_E_NULL;
+  if (B <= 0 || C <= 0 || H <= 0 || W <= 0 || C % 32) return OFLOW_E_SHAPE;
+  if ((long long)H * W * (C / 32) * 128 >= (1ll << 31)) return OFLOW_E_SHAPE;  // 32-bit row offsets per image
+  if (((reinterpret_cast<uintptr_t>(d_fmap1_s32) | reinterpret_cast<uintptr_t>(d_fmap2_s32)) & 15) != 0) return OFLOW_E_ALIGN;
+  int hl[OFLOW_MAX_LEVELS], wl[OFLOW_MAX_LEVELS];
+  int st = oflow_corr_pyramid_dims(H, W, num_levels, hl, wl);
+  if (st != OFLOW_OK) return st;
+  for (int l = 0; l < num_levels; ++l) {
+    if (hl[l] < 1 || wl[l] < 1) return OFLOW_E_TINY;
+    if (!d_levels[l]) return OFLOW_E_NULL;
+    if ((reinterpret_cast<uintptr_t>(d_levels[l]) & 3) != 0) return OFLOW_E_ALIGN;
+  }
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  PyramidArgs p{};
+  p.C = C;
+  p.H = H;
+  p.W = W;
+  p.N = H * W;
+  p.nlev = num_levels < 4 ? num_levels : 4;
+  for (int l = 0; l < 4; ++l) {
+    p.lv[l] = l < num_levels ? d_levels[l] : nullptr;
+    p.Hl[l] = l < num_levels ? hl[l] : 1;
+    p.Wl[l] = l < num_levels ? wl[l] : 1;
+    p.HB[l] = (p.Hl[l] + 3) / 4;
+    p.WB[l] = (p.Wl[l] + 7) / 8;
+  }
+  p.tiles_x = (W + kTC - 1) / kTC;
+  p.scale = sqrtf(static_cast<float>(C));
+  int e2 = 0;
+  p.scale_pow2 = (frexpf(p.scale, &e2) == 0.5f) ? 1 : 0;
+  p.inv_scale = p.scale_pow2 ? 1.0f / p.scale : 0.0f;
+  const dim3 grid(p.tiles_x * ((H + kTR - 1) / kTR), (p.N + kBM - 1) / kBM, B);
+  hipLaunchKernelGGL((corr_pyramid_s32_kernel<true>), grid, dim3(kThreads), 0, s, p,
+                     static_cast<const uint8_t*>(d_fmap1_s32), static_cast<const uint8_t*>(d_fmap2_s32));
+  st = launch_status();
+  if (st != OFLOW_OK) return st;
+  for (int l = 4; l < num_levels; ++l) {
+    const long long planes = (long long)B * p.N;
+    const long long total = planes * hl[l] * wl[l];
+    const int blocks = (int)((total + 255) / 256 < 8192 ? (total + 255) / 256 : 8192);
+    hipLaunchKernelGGL(avgpool2x2_tiled_kernel, dim3(blocks), dim3(256), 0, s, d_levels[l - 1], d_levels[l], planes,
+                       (hl[l - 1] + 3) / 4, (wl[l - 1] + 7) / 8, hl[l], wl[l], (hl[l] + 3) / 4, (wl[l] + 7) / 8);
     st = launch_status();
     if (st != OFLOW_OK) return st;
   }

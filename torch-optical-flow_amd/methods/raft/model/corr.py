@@ -42,6 +42,18 @@ class CorrBlock:
         # lookups read the tiled layout (4x8 tiles = 128-B lines); the canonical list is built on first access
         self._tiled = _native.corr_pyramid_tiled(fmap1, fmap2, num_levels)
 
+    @classmethod
+    def from_split_features(cls, f1s: Tensor, f2s: Tensor, num_levels: int = 4, radius: int = 4) -> "CorrBlock":
+        """A CorrBlock over feature maps given as S32 rows (B, H, W, C/32, 2, 32) -- the split-fp16 feature encoder's
+        output -- with the pyramid built from split-fp16 products (oflow_corr_pyramid_tiled_s32): an addition, used
+        by the RAFT forward (whose convolutions are split-fp16 already); values within the pyramid tolerance of the
+        fp32 build. Inference only."""
+        blk = cls.__new__(cls)
+        blk.num_levels, blk.radius = num_levels, radius
+        blk._pyramid, blk._grad, blk._batch = None, False, int(f1s.shape[0])
+        blk._tiled = _native.corr_pyramid_tiled_s32(f1s, f2s, num_levels)
+        return blk
+
     @property
     def corr_pyramid(self) -> List[Tensor]:
         """The reference's ``corr_pyramid``: (B*H*W, 1, H_l, W_l) fp32 per level. Materialised on first access;

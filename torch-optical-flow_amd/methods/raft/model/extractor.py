@@ -230,9 +230,12 @@ class SplitEncoder:
         _native.stem_patches(x, patches)
         return patches
 
-    def __call__(self, x: Union[Tensor, Sequence[Tensor]], patches: Optional[Tensor] = None) -> Union[Tensor, Tuple[Tensor, ...]]:
+    def __call__(self, x: Union[Tensor, Sequence[Tensor]], patches: Optional[Tensor] = None,
+                 split_out: bool = False) -> Union[Tensor, Tuple[Tensor, ...]]:
         """``patches``: the stem's patch matrix of ``x`` when another encoder already built it (RAFT's cnet reads
-        image0's rows of fnet's, raft.py:109/115); the one built here is kept as ``self.patches``."""
+        image0's rows of fnet's, raft.py:109/115); the one built here is kept as ``self.patches``. ``split_out``: the
+        head convolution writes its output as S32 rows (B, H, W, C/32, 2, 32) instead of fp32 NCHW (the RAFT forward's
+        correlation input, CorrBlock.from_split_features)."""
         is_list = isinstance(x, (tuple, list))
         if is_list:
             batch_dim = x[0].shape[0]
@@ -268,8 +271,12 @@ class SplitEncoder:
                 if out_s2d:
                     pass  # cur now holds (n, h/2, w/2, 4C) for the next stage
         head = self.w["head"]
-        out = torch.empty((n, head.n, h, w), device=dev, dtype=torch.float32)
-        _native.conv_s32(V(cur), head, self._bn(head.n), f32=out)
+        if split_out:
+            out = _native.s32_empty(n, h, w, (head.n + 31) // 32, dev)
+            _native.conv_s32(V(cur), head, self._bn(head.n), y0=V(out))
+        else:
+            out = torch.empty((n, head.n, h, w), device=dev, dtype=torch.float32)
+            _native.conv_s32(V(cur), head, self._bn(head.n), f32=out)
         if is_list:
             return torch.split(out, [batch_dim, batch_dim], dim=0)
         return out

@@ -105,6 +105,9 @@ class RAFT(nn.Module):
         # lookup fused into convc1 (csrc/corr_convc1.hip; CorrBlock, radius 3 / 4): each lane runs
         # relu(convc1(lookup)) as one kernel and the lookup volume never reaches HBM (pair_lookup then does not apply)
         self.lookup_fusion = True
+        # with the split encoders, fnet writes its features as S32 rows and the pyramid is built from split-fp16
+        # products (oflow_corr_pyramid_tiled_s32); False: fp32 features and the fp32-MFMA pyramid
+        self.split_corr = True
         # the split paths cache packed fp16 hi/lo weights keyed by (storage, version); parameters created under
         # torch.inference_mode() have no version counter, so loading new weights in place drops the caches
         for m in (self.fnet, self.cnet, self.update_block):
@@ -250,8 +253,13 @@ class RAFT(nn.Module):
                 side.wait_stream(main)
                 with torch.cuda.stream(side):
                     cnet_out = cnet(image0, patches=patches[: image0.shape[0]])
-            fmap1, fmap2 = fnet([image0, image1], patches=patches)
-            corr_fn = block(fmap1.float(), fmap2.float(), radius=self.hparams.corr_radius)
+            if block is CorrBlock and self.split_corr:
+                # features as S32 rows straight from fnet's head conv -> split-fp16 pyramid (no fp32 fmaps)
+                f1s, f2s = fnet([image0, image1], patches=patches, split_out=True)
+                corr_fn = CorrBlock.from_split_features(f1s, f2s, radius=self.hparams.corr_radius)
+            else:
+                fmap1, fmap2 = fnet([image0, image1], patches=patches)
+                corr_fn = block(fmap1.float(), fmap2.float(), radius=self.hparams.corr_radius)
             if side is not None:
                 main.wait_stream(side)
             else:

@@ -62,6 +62,7 @@ SYMBOLS = (
     "oflow_flow2rgb_f32",
     "oflow_flow_pack_f32",
     "oflow_corr_lookup_convc1_s32",
+    "oflow_corr_pyramid_tiled_s32",
 )
 
 _lib = None
@@ -177,6 +178,8 @@ def load() -> ctypes.CDLL:
     lib.oflow_corr_lookup_tiled_nhwc_f32.restype = I
     lib.oflow_corr_lookup_tiled_nhwc_f32.argtypes = [PP, IP, IP, I, P, I, I, I, I, P, I, P]
     lib.oflow_convex_upsample_f32.restype = I
+    lib.oflow_corr_pyramid_tiled_s32.restype = I
+    lib.oflow_corr_pyramid_tiled_s32.argtypes = [P, P, I, I, I, I, I, PP, P]
     lib.oflow_corr_lookup_convc1_s32.restype = I
     lib.oflow_corr_lookup_convc1_s32.argtypes = [PP, IP, IP, I, P, I, I, I, I, P, P, P, P, ctypes.c_longlong, P]
     lib.oflow_convex_upsample_f32.argtypes = [P, P, I, I, I, P, P]
@@ -303,6 +306,34 @@ def corr_pyramid_tiled(fmap1: torch.Tensor, fmap2: torch.Tensor, num_levels: int
     _no_grad_input(f2, "fmap2", what)
     levels = list(_run(what, f1.device, ops().corr_pyramid_tiled, f1, f2, int(num_levels)))
     return TiledPyramid(levels, pyramid_dims(f1.shape[2], f1.shape[3], num_levels), int(levels[0].shape[0]))
+
+
+def corr_pyramid_tiled_s32(f1: torch.Tensor, f2: torch.Tensor, num_levels: int = 4) -> TiledPyramid:
+    """The tiled pyramid from S32 feature maps (B, H, W, C/32, 2, 32) (oflow_corr_pyramid_tiled_s32: split-fp16
+    products, fp32 accumulation; the RAFT forward's pyramid)."""
+    what = "corr_pyramid"
+    for t in (f1, f2):
+        if t.dtype != torch.float16 or t.dim() != 6 or tuple(t.shape[-2:]) != (2, 32) or not t.is_contiguous():
+            raise RuntimeError(f"{what}: S32 feature maps must be contiguous fp16 (B, H, W, G, 2, 32)")
+        if t.device.type != "cuda":
+            raise RuntimeError(f"{what}: S32 feature maps must be on the GPU (no CPU fallback)")
+    if f1.shape != f2.shape or f1.device != f2.device:
+        raise RuntimeError(f"{what}: feature maps differ in shape or device")
+    b, h, w, g = (int(v) for v in f1.shape[:4])
+    dims = pyramid_dims(h, w, num_levels)
+    lib = load()
+    per_q = [int(lib.oflow_corr_tiled_level_floats(hl, wl)) for hl, wl in dims]
+    q = b * h * w
+    store = torch.empty((q * sum(per_q),), device=f1.device, dtype=torch.float32)
+    levels, off = [], 0
+    for n in per_q:
+        levels.append(store[off * q : (off + n) * q].view(q, n))
+        off += n
+    ptrs = (ctypes.c_void_p * MAX_LEVELS)(*[t.data_ptr() for t in levels])
+    with torch.cuda.device(f1.device), _Timed(what, f1.device):
+        _check(lib.oflow_corr_pyramid_tiled_s32(f1.data_ptr(), f2.data_ptr(), b, g * 32, h, w, int(num_levels), ptrs,
+                                                _stream(f1.device)), what)
+    return TiledPyramid(levels, dims, q)
 
 
 def corr_lookup_tiled(pyr: TiledPyramid, coords: torch.Tensor, radius: int) -> torch.Tensor:
