@@ -239,13 +239,19 @@ class SplitEncoder:
         is_list = isinstance(x, (tuple, list))
         if is_list:
             batch_dim = x[0].shape[0]
-            x = torch.cat(list(x), dim=0)
-        x = x.float().contiguous()
-        n, _, hh, ww = x.shape
+            n, _, hh, ww = x[0].shape
+            n *= len(x)
+            if patches is None or tuple(patches.shape[:4]) != (n, hh // 2, ww // 2, self.w["stem"].kg):
+                x = torch.cat(list(x), dim=0)  # (with the patches given the images themselves are not read)
+        if not isinstance(x, (tuple, list)):
+            x = x.float().contiguous()
+            n, _, hh, ww = x.shape
+            dev = x.device
+        else:
+            dev = x[0].device
         if hh % 8 or ww % 8:
             raise RuntimeError("SplitEncoder: H and W must be multiples of 8")
         V = _native.S32Slice
-        dev = x.device
         h, w = hh // 2, ww // 2
         if patches is None or tuple(patches.shape[:4]) != (n, h, w, self.w["stem"].kg):
             patches = _native.s32_empty(n, h, w, self.w["stem"].kg, dev)
