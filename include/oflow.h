@@ -232,7 +232,8 @@ int oflow_corr_lookup_convc1_s32(const float* const* d_levels, const int* level_
  *   out_groups) with channel t*C + c (t = ky*7 + kx), zeros past 49*C.
  * oflow_norm_stats_finalize: merge the partials (fp64 sums) -> alpha = 1/sqrt(var + eps), beta = -mean * alpha, [B][C].
  * oflow_norm_apply_s32: y = act(x*alpha + beta) for x [P][C] fp32 (C % 8 == 0); res_mode 1: y = res_act(y + S32 res),
- *   res_mode 2: y = res_act((x2*alpha2 + beta2) + y); written as S32 (s2d: space-to-depth as above).
+ *   res_mode 2: y = res_act((x2*alpha2 + beta2) + y); res_mode 3: y = res_act(relu(x2*alpha2 + beta2) + y) (a block
+ *   input kept as raw fp32 + its norm); written as S32 (s2d: space-to-depth as above).
  */
 int oflow_conv_s32_ex(const void* d_x, long long x_pixel_stride, int in_groups, const void* d_wpack, int n_pad,
                       const float* d_wscale, const float* d_bias, int N, int B, int H, int W, int kh, int kw,

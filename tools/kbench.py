@@ -57,6 +57,9 @@ def main():
     del pyr
     torch.cuda.empty_cache()
     pm = timed(lambda: _native.corr_pyramid(f1, f2, 4), args.iters)
+    s1, s2 = _native.s32_from_f32(f1), _native.s32_from_f32(f2)
+    pms = timed(lambda: _native.corr_pyramid_tiled_s32(s1, s2, 4), args.iters)  # the RAFT forward's split-fp16 build
+    del s1, s2
     pyr = _native.corr_pyramid(f1, f2, 4)
     lm_canon = timed(lambda: _native.corr_lookup(pyr, coords, 4), args.iters * 5)
     del pyr
@@ -77,6 +80,8 @@ def main():
         json.dumps(
             {
                 "shape": args.shape,
+                "pyramid_s32_ms": round(pms, 5),
+                "pyramid_s32_f16_tflops": round(3 * pyramid_cost(b, dims)[0] / pms / 1e9, 2),
                 "pyramid_ms": round(pm, 4),
                 "pyramid_tflops": round(flops / pm / 1e9, 2),
                 "pyramid_GBs": round(pbytes / pm / 1e6, 1),

@@ -186,14 +186,19 @@ __global__ __launch_bounds__(256) void norm_apply_kernel(const float* __restrict
     const half8 rh = *reinterpret_cast<const half8*>(rl), rlo = *reinterpret_cast<const half8*>(rl + 64);
 #pragma unroll
     for (int j = 0; j < 8; ++j) v[j] = act_fn(v[j] + (static_cast<float>(rh[j]) + static_cast<float>(rlo[j])), res_act);
-  } else if (res_mode == 2) {  // normalised raw residual (downsample branch: norm3(conv1x1(x)))
+  } else if (res_mode >= 2) {  // normalised raw residual: 2 = the downsample branch norm3(conv1x1(x)); 3 = a block
+                                // input kept raw, relu(norm(x)) (the stem's output feeding layer1's first block)
     const float4* rp = reinterpret_cast<const float4*>(x2 + p * C + c0);
     const float4 r0 = rp[0], r1 = rp[1];
     const float r[8] = {r0.x, r0.y, r0.z, r0.w, r1.x, r1.y, r1.z, r1.w};
     const float* a2 = alpha2 + (long long)b * C + c0;
     const float* b2 = beta2 + (long long)b * C + c0;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) v[j] = act_fn((r[j] * a2[j] + b2[j]) + v[j], res_act);
+    for (int j = 0; j < 8; ++j) {
+      float rn = r[j] * a2[j] + b2[j];
+      if (res_mode == 3) rn = act_fn(rn, 1);
+      v[j] = act_fn(rn + v[j], res_act);
+    }
   }
   long long pd = p;
   int cd = c0;
@@ -247,10 +252,10 @@ extern "C" int oflow_norm_apply_s32(const float* d_x, int C, int B, int H, int W
                                     long long y_pixel_stride, void* stream) {
   if (!d_x || !d_alpha || !d_beta || !d_y) return OFLOW_E_NULL;
   if (B <= 0 || C <= 0 || C % 8 || H <= 0 || W <= 0) return OFLOW_E_SHAPE;
-  if (activation < 0 || activation > 3 || res_activation < 0 || res_activation > 3 || res_mode < 0 || res_mode > 2)
+  if (activation < 0 || activation > 3 || res_activation < 0 || res_activation > 3 || res_mode < 0 || res_mode > 3)
     return OFLOW_E_MODE;
   if (res_mode == 1 && !d_res) return OFLOW_E_NULL;
-  if (res_mode == 2 && (!d_x2 || !d_alpha2 || !d_beta2)) return OFLOW_E_NULL;
+  if (res_mode >= 2 && (!d_x2 || !d_alpha2 || !d_beta2)) return OFLOW_E_NULL;
   if (s2d && ((H | W) & 1)) return OFLOW_E_SHAPE;
   if (((uintptr_t)d_x & 15) || ((uintptr_t)d_y & 15) || (y_pixel_stride & 127) ||
       (d_res && (((uintptr_t)d_res & 15) || (res_pixel_stride & 127))) || (d_x2 && ((uintptr_t)d_x2 & 15)))

@@ -199,7 +199,10 @@ class SplitEncoder:
                 return raw, alpha, beta
             if out is None:
                 out = _native.s32_empty(b, h // 2 if s2d else h, w // 2 if s2d else w, (cw.n * (4 if s2d else 1) + 31) // 32, dev)
-            if isinstance(res, tuple):
+            if isinstance(res, _native.NhwcNormIn):  # a block input kept raw: relu(norm(x)) + y
+                _native.norm_apply(raw, (b, cw.n, h, w), alpha, beta, act, V(out), res_raw=(res.raw, res.scale, res.shift),
+                                   res_act="relu", s2d=s2d, res_raw_relu=True)
+            elif isinstance(res, tuple):
                 _native.norm_apply(raw, (b, cw.n, h, w), alpha, beta, act, V(out), res_raw=res, res_act="relu", s2d=s2d)
             else:
                 _native.norm_apply(raw, (b, cw.n, h, w), alpha, beta, act, V(out), res=res, res_act="relu" if res is not None else "none", s2d=s2d)
@@ -257,7 +260,10 @@ class SplitEncoder:
             patches = _native.s32_empty(n, h, w, self.w["stem"].kg, dev)
             _native.stem_patches(x, patches)
         self.patches = patches
-        cur = self._conv_norm(V(patches), self.w["stem"], (n, h, w), "relu")
+        # instance norm: the stem's output stays raw fp32 + its norm (relu(norm(.)) applied by layer1's first conv while
+        # it stages its input, and by that block's residual tail): no normalised copy is written
+        cur = (self._conv1(V(patches), self.w["stem"], (n, h, w)) if self.inorm
+               else self._conv_norm(V(patches), self.w["stem"], (n, h, w), "relu"))
         layers = (self.enc.layer1, self.enc.layer2, self.enc.layer3)
         for li, layer in enumerate(layers):
             for bi, blk in enumerate(layer):
@@ -265,8 +271,9 @@ class SplitEncoder:
                 out_s2d = last_of_stage and li + 1 < len(layers)  # the next stage starts with stride-2 convs
                 pre = f"{li}.{bi}."
                 if blk.downsample is None:
-                    t = self._conv1(V(cur), self.w[pre + "conv1"], (n, h, w))
-                    cur = self._conv_norm(t, self.w[pre + "conv2"], (n, h, w), "relu", res=V(cur), s2d=out_s2d)
+                    x_in = cur if isinstance(cur, _native.NhwcNormIn) else V(cur)
+                    t = self._conv1(x_in, self.w[pre + "conv1"], (n, h, w))
+                    cur = self._conv_norm(t, self.w[pre + "conv2"], (n, h, w), "relu", res=x_in, s2d=out_s2d)
                 else:
                     h, w = h // 2, w // 2  # cur is the space-to-depth input at the new resolution
                     t = self._conv1(V(cur), self.w[pre + "conv1"], (n, h, w))

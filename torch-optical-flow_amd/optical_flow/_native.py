@@ -848,16 +848,16 @@ def norm_stats(partials: torch.Tensor, b: int, tiles: int, n_pad: int, c: int, e
 
 
 def norm_apply(x: torch.Tensor, shape, alpha, beta, act: str, y: S32Slice, res=None, res_raw=None, res_act: str = "none",
-               s2d: bool = False) -> None:
+               s2d: bool = False, res_raw_relu: bool = False) -> None:
     """y = act(x*alpha + beta) (+ residual, res_act) as S32. x: [P, C] fp32 (NHWC). res: S32Slice (identity shortcut);
-    res_raw: (x2 [P, C], alpha2, beta2) normalised shortcut."""
+    res_raw: (x2 [P, C], alpha2, beta2) normalised shortcut (relu'd first when res_raw_relu)."""
     b, c, h, w = shape
     mode, rp, rps = 0, None, 0
     x2 = a2 = b2 = None
     if res is not None:
         mode, rp, rps = 1, res.ptr, res.ps
     elif res_raw is not None:
-        mode = 2
+        mode = 3 if res_raw_relu else 2
         x2, a2, b2 = (t.data_ptr() for t in res_raw)
     with torch.cuda.device(x.device), _Timed("norm_apply", x.device):
         _check(
