@@ -138,10 +138,15 @@ __device__ __forceinline__ void gemm_tile(int Mt, int Nt, int& tile, int& qblk) 
   qblk = band * kGM + (in_band - (in_band / rows) * rows);
 }
 
+// level-0 staging: tiles 2, 3 of a tile row swap their row pairs (bit 3 of the float offset) so that the 32 lanes of
+// one accumulator row write 32 different banks (tiles 0 and 2 are 64 floats apart); 16-B chunks stay whole
+__device__ __forceinline__ int l0swz(int e) { return e ^ (((e >> 6) & 1) << 3); }
+
 // Epilogue shared by the fp32 and split-fp16 kernels (both leave the same 32x32 C/D accumulator map): scale by 1/sqrt(C),
 // level-0 store, levels 1..3 pooled in registers.
 template <bool TILED>
-__device__ __forceinline__ void pyramid_epilogue(const PyramidArgs& p, f32x16 (&acc)[kTR], int i0, int ty0, int tx0, int b) {
+__device__ __forceinline__ void pyramid_epilogue(const PyramidArgs& p, f32x16 (&acc)[kTR], int i0, int ty0, int tx0, int b,
+                                                 float* sbuf) {
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
   // ---- epilogue: scale, level-0 store, in-register pooled levels 1..3 ----
@@ -154,7 +159,38 @@ __device__ __forceinline__ void pyramid_epilogue(const PyramidArgs& p, f32x16 (&
     for (int r = 0; r < 16; ++r) acc[n][r] = p.scale_pow2 ? acc[n][r] * p.inv_scale : acc[n][r] / p.scale;
   }
 
-  {  // level 0: (B*N, H, W)
+  if constexpr (TILED) {
+    // level 0 through LDS as whole tiles: a wave's 32 queries x (8 rows x 32 cols) are, per query, 2 tile rows x 4
+    // 4x8 tiles = 2 runs of 512 contiguous bytes of the tiled level. Four passes of 8 queries: the accumulators go to
+    // the wave's 8 KB of LDS in the tiled byte order, then each lane stores 16-B chunks, a wave instruction writing
+    // 2 x 512 B (whole 128-B lines) instead of 8 scattered 32-B row pieces.
+    float* sw = sbuf + wave * 2048;
+    const int tb = p.WB[0] - (tx0 >> 3);  // tiles of this tile row that exist in the level (>= 1)
+    __syncthreads();  // the main loop's LDS operand reads are done (the scratch aliases them)
+#pragma unroll
+    for (int ps = 0; ps < 4; ++ps) {
+#pragma unroll
+      for (int n = 0; n < kTR; ++n)
+#pragma unroll
+        for (int k = 0; k < 4; ++k)  // query wave*32 + 8ps + k + 4hh <- acc[n][4ps + k]
+          sw[(k + 4 * (lane >> 5)) * 256 + l0swz((n >> 2) * 128 + (tx >> 3) * 32 + (n & 3) * 8 + (tx & 7))] = acc[n][4 * ps + k];
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      const int tr = lane >> 5, ch = lane & 31;  // tile row, 16-B chunk of its 512 B
+      const int y0 = ty0 + 4 * tr;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int i = i0 + wave * 32 + 8 * ps + j;
+        const float4 v = *reinterpret_cast<const float4*>(&sw[j * 256 + l0swz(tr * 128 + ch * 4)]);
+        if (i < p.N && (y0 >> 2) < p.HB[0] && (ch >> 3) < tb)
+          *reinterpret_cast<float4*>(&p.lv[0][lvl_off<true>(p, 0, (size_t)b * Nn + i, y0, tx0) + ch * 4]) = v;
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();  // every lane's reads of this pass are done before the next pass overwrites
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    }
+  } else {  // level 0: (B*N, H, W)
     float* L0 = p.lv[0];
     const int gx = tx0 + tx;
 #pragma unroll
@@ -190,7 +226,13 @@ __device__ __forceinline__ void pyramid_epilogue(const PyramidArgs& p, f32x16 (&
         const float a0 = acc[2 * m][r], c0 = acc[2 * m + 1][r];
         v1[h][r] = pool4(a0, dpp_xor1(a0), c0, dpp_xor1(c0));
         const int i = qbase + (r & 3) + 8 * (r >> 2);
-        if (ok && i < p.N) p.lv[1][lvl_off<TILED>(p, 1, (size_t)b * Nn + i, y1, x1)] = v1[h][r];
+        if constexpr (TILED) {
+          // staged: this wave's 32 queries x (4 rows x 16 cols) = per query one tile row of 2 tiles (256 B)
+          if ((tx & 1) == 0)
+            sbuf[wave * 2048 + ((r & 3) + 8 * (r >> 2) + 4 * (lane >> 5)) * 64 + (tx >> 4) * 32 + m * 8 + ((tx >> 1) & 7)] = v1[h][r];
+        } else {
+          if (ok && i < p.N) p.lv[1][lvl_off<TILED>(p, 1, (size_t)b * Nn + i, y1, x1)] = v1[h][r];
+        }
       }
     }
     if (p.nlev >= 3) {
@@ -203,6 +245,21 @@ __device__ __forceinline__ void pyramid_epilogue(const PyramidArgs& p, f32x16 (&
         const int i = qbase + (r & 3) + 8 * (r >> 2);
         if (ok && i < p.N) p.lv[2][lvl_off<TILED>(p, 2, (size_t)b * Nn + i, y2, x2)] = v2[pr][r];
       }
+    }
+  }
+  if constexpr (TILED) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    const float* sw = sbuf + wave * 2048;
+    const int y1 = ty0 >> 1, tb1 = p.WB[1] - (tx0 >> 4), ch = lane & 15;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int ql = 4 * j + (lane >> 4);
+      const int i = i0 + wave * 32 + ql;
+      const float4 v = *reinterpret_cast<const float4*>(&sw[ql * 64 + ch * 4]);
+      if (i < p.N && (y1 >> 2) < p.HB[1] && (ch >> 3) < tb1)
+        *reinterpret_cast<float4*>(&p.lv[1][lvl_off<true>(p, 1, (size_t)b * Nn + i, y1, tx0 >> 1) + ch * 4]) = v;
     }
   }
   if (p.nlev < 4) return;
@@ -266,7 +323,7 @@ __global__ __launch_bounds__(kThreads, 2) void corr_pyramid_kernel(PyramidArgs p
     __syncthreads();
   }
 
-  pyramid_epilogue<TILED>(p, acc, i0, ty0, tx0, b);
+  pyramid_epilogue<TILED>(p, acc, i0, ty0, tx0, b, &sB[0][0][0]);
 }
 
 // ---------------------------------------------------------------------------------------------------------------
@@ -366,7 +423,7 @@ __global__ __launch_bounds__(kThreads, 2) void corr_pyramid_s32_kernel(PyramidAr
       }
     }
   }
-  pyramid_epilogue<TILED>(p, acc, i0, ty0, tx0, b);
+  pyramid_epilogue<TILED>(p, acc, i0, ty0, tx0, b, reinterpret_cast<float*>(sB));
 }
 
 // Levels >= 4 (num_levels > 4 only): plain floor 2x2 average pool of the level above.
