@@ -157,3 +157,16 @@ def test_raft_fused_lanes_deterministic_on_dirty_memory():
     for o in outs:
         assert bool(torch.isfinite(o).all())
         assert torch.equal(o, outs[0])
+
+
+def test_raft_fnet_streams_bit_identical():
+    """fnet's two images on two streams (RAFT.fnet_streams) = one 2B batch, bit for bit (instance norm is per image)."""
+    img0, img1 = synthetic.synthetic_pair(3, 128, 256, seed=8)
+    img0, img1 = img0.to(DEV), img1.to(DEV)
+    model = _raft(True)
+    outs = []
+    for fs in (True, False):
+        model.fnet_streams = fs
+        with torch.inference_mode():
+            outs.append(model(img0, img1, iters=6, test_mode=True)[1])
+    assert torch.equal(outs[0], outs[1])

@@ -97,6 +97,7 @@ class RAFT(nn.Module):
         # "split": encoders on the split-fp16 kernels (SplitEncoder) in GPU inference; "module": nn.Module (MIOpen)
         self.encoder_impl = "split"
         self.encoder_streams = True  # cnet beside fnet + the corr pyramid (inference, split encoders)
+        self.fnet_streams = True  # with encoder_streams: fnet's image0 and image1 halves on two streams
         # split update loop over >= 2 pairs (CorrBlock): the pairs' two halves run on two streams so that one half's
         # convolutions fill the CUs the other half's leave idle at a wave tail. pair_lookup "joined": one full-batch
         # lookup per iteration on the main stream (both halves joined around it); "lane": each half looks up its own.
@@ -246,16 +247,31 @@ class RAFT(nn.Module):
         if split_enc and isinstance(cnet, SplitEncoder):
             # image0's stem patches are the first rows of fnet's (raft.py:109, 115 feed both the same image0); cnet
             # runs on a side stream beside fnet and the correlation pyramid, joined before the update loop
-            patches = fnet.stem_patches(torch.cat([image0, image1], dim=0))
             main = torch.cuda.current_stream(image0.device)
             side = _side_stream(image0.device) if self.encoder_streams else None
+            nb = image0.shape[0]
+            side2 = (_side_stream(image0.device, 1) if side is not None and self.fnet_streams
+                     and block is CorrBlock and self.split_corr else None)
+            if side2 is not None:
+                # fnet's two images on two streams, each building its own stem patches (instance norm is per image:
+                # the same values as one batch), so three 8-image encoders share the chip and finish together
+                side2.wait_stream(main)
+                with torch.cuda.stream(side2):
+                    f2s = fnet(image1, split_out=True)
+                patches = fnet.stem_patches(image0)
+            else:
+                patches = fnet.stem_patches(torch.cat([image0, image1], dim=0))
             if side is not None:
                 side.wait_stream(main)
                 with torch.cuda.stream(side):
-                    cnet_out = cnet(image0, patches=patches[: image0.shape[0]])
+                    cnet_out = cnet(image0, patches=patches[:nb])
             if block is CorrBlock and self.split_corr:
                 # features as S32 rows straight from fnet's head conv -> split-fp16 pyramid (no fp32 fmaps)
-                f1s, f2s = fnet([image0, image1], patches=patches, split_out=True)
+                if side2 is not None:
+                    f1s = fnet(image0, patches=patches, split_out=True)
+                    main.wait_stream(side2)
+                else:
+                    f1s, f2s = fnet([image0, image1], patches=patches, split_out=True)
                 corr_fn = CorrBlock.from_split_features(f1s, f2s, radius=self.hparams.corr_radius)
             else:
                 fmap1, fmap2 = fnet([image0, image1], patches=patches)
