@@ -603,8 +603,20 @@ int launch_conv(const ConvArgs& a0, hipStream_t s) {
   return launch_status();
 }
 
+// Small grids (batch 1 and other small images: under 16384 output pixels, e.g. every update-block conv of one Sintel
+// pair launches 28-112 workgroups on 256 CUs at the default tiles): 2-row x 32-column tiles and 64-channel blocks, up
+// to 4x the workgroups. Same k order per output element, so the results are bit-identical to the default tiles.
+// In-process A/B (tools/exp/run_small_grid_ab.py): batch 1 x 24 iterations 12.9 -> 8.8 ms; a pixel threshold keeps
+// the 4-pair lanes of the 8-pair step (28160 px) on the default tiles, where the small ones cost +1.5-3 %.
+int g_small_grid_px = 16384;  // output-pixel count under which the small tiles are used (0: never; experiments only)
+inline bool small_grid(const ConvArgs& a, int bn) {
+  return (long long)a.B * a.H * a.W < g_small_grid_px && a.stats == nullptr && a.ain == kInS32 && a.npad % 64 == 0 &&
+         bn >= 64;
+}
+
 template <int KH, int KW, int EPI>
 int launch_bn(const ConvArgs& a, int bn, hipStream_t s) {
+  if (small_grid(a, bn)) return launch_conv<KH, KW, 64, 2, 2, EPI, 2>(a, s);
   switch (bn) {
     case 128: return launch_conv<KH, KW, 128, 2, 2, EPI>(a, s);
     case 96: return launch_conv<KH, KW, 96, 4, 1, EPI>(a, s);
@@ -634,11 +646,19 @@ int dispatch_conv(const ConvArgs& a, int kh, int kw, int block_n, int epilogue, 
       }
     case 1:
       if (block_n != 128) return OFLOW_E_SHAPE;
+      if (small_grid(a, block_n)) {
+        if (key == 0x15) return launch_conv<1, 5, 64, 2, 2, 1, 2>(a, s);
+        if (key == 0x51) return launch_conv<5, 1, 64, 2, 2, 1, 2>(a, s);
+      }
       if (key == 0x15) return launch_conv<1, 5, 128, 2, 2, 1>(a, s);
       if (key == 0x51) return launch_conv<5, 1, 128, 2, 2, 1>(a, s);
       return OFLOW_E_SHAPE;
     default:
       if (block_n != 128) return OFLOW_E_SHAPE;
+      if (small_grid(a, block_n)) {
+        if (key == 0x15) return launch_conv<1, 5, 64, 2, 2, 2, 2>(a, s);
+        if (key == 0x51) return launch_conv<5, 1, 64, 2, 2, 2, 2>(a, s);
+      }
       if (key == 0x15) return launch_conv<1, 5, 128, 2, 2, 2>(a, s);
       if (key == 0x51) return launch_conv<5, 1, 128, 2, 2, 2>(a, s);
       return OFLOW_E_SHAPE;
@@ -779,3 +799,6 @@ extern "C" int oflow_conv_s32(const void* d_x, long long x_pixel_stride, int in_
                            d_f32, f32_batch_stride, f32_channel_stride, f32_accumulate, d_gru_h, d_gru_z, gru_channels,
                            nullptr, 0, nullptr, nullptr, 0, 0, 0, stream);
 }
+
+// experiment hook (not part of include/oflow.h): the small-grid pixel threshold, for in-process A/B runs (tools/exp)
+extern "C" void oflow_exp_set_small_grid_px(int pixels) { oflow::g_small_grid_px = pixels; }
