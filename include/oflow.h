@@ -190,6 +190,12 @@ int oflow_pack_s32_f32(const float* d_x, long long x_batch_stride, int C, int B,
                        float* d_nhwc, int nhwc_pixel_stride, void* stream);
 int oflow_flow_prep_s32(const float* d_coords, int B, int H, int W, void* d_patches, void* d_flow0,
                         long long flow0_pixel_stride, void* d_flow1, long long flow1_pixel_stride, void* stream);
+/* oflow_flow_head2_s32: the flow head's output conv (update.py:35-36 conv2: 3x3, C -> 2, zero padding) added into
+ * coords (B, 2, H, W) fp32 in place (raft.py:133 `coords1 = coords1 + delta_flow`), from an S32 input of in_groups
+ * groups (1..8): fp32 FMAs on the exact S32 values; d_weight (2, C, 3, 3) fp32 as the nn.Conv2d stores it, d_bias [2].
+ * Built for small grids (one image at 1/8 resolution); larger ones run faster as oflow_conv_s32 with n_pad 32. */
+int oflow_flow_head2_s32(const void* d_x, long long x_pixel_stride, int in_groups, const float* d_weight,
+                         const float* d_bias, int B, int H, int W, float* d_coords, void* stream);
 /* oflow_corr_lookup_tiled_nhwc_f32: the tiled lookup as fp32 NHWC rows [B*H*W][row_floats] (d_out 16-B aligned) in the
  * reference's channel order: row q, channel l*(2r+1)^2 + k = oflow_corr_lookup_tiled_f32's (b, l*(2r+1)^2 + k, y, x) bit for
  * bit; row_floats >= num_levels*(2r+1)^2, channels past that are not written. With row_floats = num_levels*(2r+1)^2 (324)

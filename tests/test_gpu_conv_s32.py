@@ -288,3 +288,36 @@ def test_range_check_fires_on_fp16_overflow(monkeypatch):
         N.conv_s32(N.NhwcNormIn(rows.clamp(-10, 10), b, h, w, scale, shift), cw3, 32, f32=out)
     monkeypatch.setattr(N, "CHECK_RANGE", False)
     N.conv_s32(N.S32Slice(N.s32_from_f32(big)), cw, 32, f32=out)  # off: no check, no raise
+
+
+@pytest.mark.parametrize("b,h,w", [(2, 55, 128), (1, 7, 9), (3, 16, 33)])
+def test_flow_head2_matches_fp64(b, h, w):
+    """The flow head's 2-channel output conv as fp32 FMAs (oflow_flow_head2_s32) added into coords, vs float64; the
+    small grids put most pixels on the zero-padded border."""
+    g = torch.Generator().manual_seed(h * w)
+    x = (torch.randn(b, 256, h, w, generator=g) * 1.5).to(DEV)
+    wt = (torch.randn(2, 256, 3, 3, generator=g) / 48.0).to(DEV)
+    bias = torch.randn(2, generator=g).to(DEV)
+    xs = N.s32_from_f32(x)
+    xr = N.s32_to_f32(xs, 256)
+    coords = torch.randn(b, 2, h, w, generator=g).to(DEV)
+    ref = coords.double() + F.conv2d(xr.double(), wt.double(), bias.double(), padding=1)
+    bound = F.conv2d(xr.double().abs(), wt.double().abs(), None, padding=1)
+    N.flow_head2(N.S32Slice(xs), wt.contiguous(), bias, coords)
+    torch.cuda.synchronize()
+    err = (coords.double() - ref).abs()
+    tol = 2e-6 * bound + 1e-6 + 2.0 ** -23 * ref.abs()
+    assert bool((err <= tol).all()), float(err.max())
+
+
+def test_flow_head2_arg_errors():
+    xs = N.s32_empty(1, 8, 8, 8, DEV)
+    coords = torch.zeros(1, 2, 8, 8, device=DEV)
+    conv = torch.nn.Conv2d(256, 2, 3, padding=1).to(DEV)
+    wt, bias = conv.weight.detach().contiguous(), conv.bias.detach()
+    with pytest.raises(RuntimeError):
+        N.flow_head2(N.S32Slice(xs), wt[:, :128].contiguous(), bias, coords)  # channel count must match the slice
+    with pytest.raises(RuntimeError):
+        N.flow_head2(N.S32Slice(xs), wt, None, coords)  # bias required
+    with pytest.raises(RuntimeError):
+        N.flow_head2(N.S32Slice(xs), wt, bias, coords[:, :, :4])

@@ -118,6 +118,92 @@ __global__ __launch_bounds__(256) void flow_prep_kernel(const float* __restrict_
   }
 }
 
+// Flow head output conv (update.py:35-36, `self.conv2`: 3x3, 256 -> 2, + coords1 in place, raft.py:133) for small
+// grids. Two output channels fill a matrix-core tile 1/16 (oflow_conv_s32 pads them to N = 32) and that conv's
+// LDS-staged K loop is latency-bound when the grid is one image (24.8 us at 55x128), so here the conv runs as fp32
+// FMAs with one memory round trip: a workgroup covers 32 pixels x 32 chunks of 8 channels, lane l of wave w taking
+// pixel l & 31 and chunk 2w + (l >> 5), and issues all 18 of its loads (the chunk's hi and lo 16-B slots of the 9
+// neighbours) plus its share of the weights at once. x = hi + lo exactly and the conv is linear, so hi and lo meet
+// the same fp32 weight (staged tap-major in LDS), packed two outputs per FMA. The 32 partial sums per pixel meet in
+// LDS in a fixed order. Every pixel reads its neighbours' lines 9 times (through L1/L2), which is why large grids stay
+// on oflow_conv_s32 (13 us vs 25 us at 55x128, but no faster at 4 x 55x128).
+constexpr int kFhPx = 32;
+__global__ __launch_bounds__(1024) void flow_head2_kernel(const uint8_t* __restrict__ x, long long xps, int G, int B, int H,
+                                                          int W, const float* __restrict__ w, const float* __restrict__ bias,
+                                                          float* __restrict__ coords) {
+  typedef _Float16 half8 __attribute__((ext_vector_type(8)));
+  typedef float f2 __attribute__((ext_vector_type(2)));
+  __shared__ float2 sw[9 * 256];     // [tap][channel] (w_out0, w_out1)
+  __shared__ float2 red[32][kFhPx];  // [chunk][pixel]
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int C = G * 32;
+  const int HW = H * W, P = B * HW;  // < 2^31: checked at the entry
+  const int px = lane & (kFhPx - 1);
+  const int k = (tid >> 6) * 2 + (lane >> 5);  // chunk: channels 8k .. 8k+7, group k / 4, slot k % 4
+  const int p = blockIdx.x * kFhPx + px;
+  const int pc = p < P ? p : P - 1;
+  const int b = pc / HW;
+  const int pix = pc - b * HW;
+  const int y = pix / W, xx = pix - y * W;
+  float v[5];  // this thread's weights, loaded before the neighbours and stored to LDS after them
+#pragma unroll
+  for (int j = 0; j < 5; ++j) {
+    const int i = tid + j * 1024;
+    v[j] = w[i < 2 * C * 9 ? i : 0];
+  }
+  half8 hv[9], lv[9];
+  if (k < G * 4) {
+    const uint8_t* base = x + (long long)b * HW * xps + (k >> 2) * 128 + (k & 3) * 16;
+#pragma unroll
+    for (int t = 0; t < 9; ++t) {
+      const int ny = y + t / 3 - 1, nx = xx + t % 3 - 1;  // zero padding: load the clamped neighbour, then zero it
+      const bool ok = static_cast<unsigned>(ny) < static_cast<unsigned>(H) && static_cast<unsigned>(nx) < static_cast<unsigned>(W);
+      const uint8_t* line = base + ((long long)min(max(ny, 0), H - 1) * W + min(max(nx, 0), W - 1)) * xps;
+      hv[t] = *reinterpret_cast<const half8*>(line);
+      lv[t] = *reinterpret_cast<const half8*>(line + 64);
+      if (!ok) {
+        hv[t] = half8{};
+        lv[t] = half8{};
+      }
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < 5; ++j) {  // (o, c, t) as nn.Conv2d stores the weight -> [t][c].o
+    const int i = tid + j * 1024;
+    if (i >= 2 * C * 9) break;
+    const int o = i >= C * 9, r = i - o * C * 9, c = r / 9, t = r - c * 9;
+    reinterpret_cast<float*>(sw)[(t * C + c) * 2 + o] = v[j];
+  }
+  __syncthreads();
+  f2 ah = {0.f, 0.f}, al = {0.f, 0.f};  // (out0, out1) over the hi and the lo halves
+  if (k < G * 4) {
+#pragma unroll
+    for (int t = 0; t < 9; ++t)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float2 u = sw[t * C + k * 8 + e];
+        const f2 uw = {u.x, u.y};
+        const float h = static_cast<float>(hv[t][e]), l = static_cast<float>(lv[t][e]);
+        ah = __builtin_elementwise_fma(f2{h, h}, uw, ah);
+        al = __builtin_elementwise_fma(f2{l, l}, uw, al);
+      }
+  }
+  red[k][px] = make_float2(ah.x + al.x, ah.y + al.y);
+  __syncthreads();
+  if (tid < 2 * kFhPx) {
+    const int q = tid & (kFhPx - 1), o = tid >> 5;
+    const int pq = blockIdx.x * kFhPx + q;
+    if (pq < P) {
+      const float* rf = reinterpret_cast<const float*>(&red[0][q]) + o;
+      float s = 0.f;
+#pragma unroll
+      for (int j = 0; j < 32; ++j) s += rf[j * kFhPx * 2];
+      const int bq = pq / HW;
+      coords[(long long)bq * 2 * HW + (long long)o * HW + (pq - bq * HW)] += s + bias[o];
+    }
+  }
+}
+
 }  // namespace
 }  // namespace oflow
 
@@ -149,5 +235,18 @@ extern "C" int oflow_flow_prep_s32(const float* d_coords, int B, int H, int W, v
   hipLaunchKernelGGL(flow_prep_kernel, dim3((unsigned)((items + 255) / 256)), dim3(256), 0, static_cast<hipStream_t>(stream),
                      d_coords, B, H, W, static_cast<uint8_t*>(d_patches), static_cast<uint8_t*>(d_flow0),
                      flow0_pixel_stride, static_cast<uint8_t*>(d_flow1), flow1_pixel_stride);
+  return launch_status();
+}
+
+extern "C" int oflow_flow_head2_s32(const void* d_x, long long x_pixel_stride, int in_groups, const float* d_weight,
+                                    const float* d_bias, int B, int H, int W, float* d_coords, void* stream) {
+  if (!d_x || !d_weight || !d_bias || !d_coords) return OFLOW_E_NULL;
+  if (B <= 0 || H <= 0 || W <= 0 || in_groups <= 0 || in_groups > 8 || (long long)B * H * W >= (1LL << 31))
+    return OFLOW_E_SHAPE;
+  if ((x_pixel_stride & 127) || ((uintptr_t)d_x & 15) || x_pixel_stride < 128LL * in_groups) return OFLOW_E_ALIGN;
+  const long long P = (long long)B * H * W;
+  hipLaunchKernelGGL(flow_head2_kernel, dim3((unsigned)((P + kFhPx - 1) / kFhPx)), dim3(1024), 0,
+                     static_cast<hipStream_t>(stream), static_cast<const uint8_t*>(d_x), x_pixel_stride, in_groups, B, H, W,
+                     d_weight, d_bias, d_coords);
   return launch_status();
 }

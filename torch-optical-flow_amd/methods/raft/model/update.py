@@ -257,6 +257,8 @@ class SplitUpdate:
             "mo": CW(enc.conv.weight, enc.conv.bias, 128),
             "fh1": CW(fh.conv1.weight, fh.conv1.bias, 256),
             "fh2": CW(fh.conv2.weight, fh.conv2.bias, 32),
+            # small grids: the 2-channel output conv as fp32 FMAs (oflow_flow_head2_s32) on the conv's own weights
+            "fh2_f32": (fh.conv2.weight.detach().float().contiguous(), fh.conv2.bias.detach().float().contiguous()),
             "m1": CW(block.mask[0].weight, block.mask[0].bias, 256),
             "m2": CW(block.mask[2].weight, block.mask[2].bias, 576),
         }
@@ -333,7 +335,10 @@ class SplitUpdate:
             conv(V(self.rhx), w["q" + tag], 128, epilogue=2, y0=V(self.hx, 0, 4), gru_h=self.hm, gru_z=self.z)
         net = V(self.hx, 0, 4)
         conv(net, w["fh1"], 128, "relu", y0=V(self.fh))
-        conv(V(self.fh), w["fh2"], 32, f32=coords1, f32_accumulate=True)
+        if coords1.is_contiguous() and coords1.numel() // 2 < _native.FLOW_HEAD2_MAX_PIXELS:
+            _native.flow_head2(V(self.fh), *w["fh2_f32"], coords1)  # coords1 += conv2(.) (raft.py:133)
+        else:
+            conv(V(self.fh), w["fh2"], 32, f32=coords1, f32_accumulate=True)
         if not need_mask:
             return None
         mask = mask_out if mask_out is not None else torch.empty((b, 576, h, wd), device=coords1.device, dtype=torch.float32)

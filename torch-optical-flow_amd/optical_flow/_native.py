@@ -23,6 +23,9 @@ _LIB_PATH = os.environ.get(
 ABI_VERSION = 1
 MAX_LEVELS = 8
 MAX_RADIUS = 7
+# grids below this many pixels run the flow head output conv as oflow_flow_head2_s32 (fp32 FMAs), larger ones as
+# oflow_conv_s32 (faster once the grid fills the chip): the threshold of the conv's small-grid tiles (conv_s32.hip)
+FLOW_HEAD2_MAX_PIXELS = 16384
 E_TINY = -4
 
 INTERP = {"bilinear": 0, "nearest": 1, "bicubic": 2}
@@ -63,6 +66,7 @@ SYMBOLS = (
     "oflow_flow_pack_f32",
     "oflow_corr_lookup_convc1_s32",
     "oflow_corr_pyramid_tiled_s32",
+    "oflow_flow_head2_s32",
 )
 
 _lib = None
@@ -178,6 +182,8 @@ def load() -> ctypes.CDLL:
     lib.oflow_corr_lookup_tiled_nhwc_f32.restype = I
     lib.oflow_corr_lookup_tiled_nhwc_f32.argtypes = [PP, IP, IP, I, P, I, I, I, I, P, I, P]
     lib.oflow_convex_upsample_f32.restype = I
+    lib.oflow_flow_head2_s32.restype = I
+    lib.oflow_flow_head2_s32.argtypes = [P, ctypes.c_longlong, I, P, P, I, I, I, P, P]
     lib.oflow_corr_pyramid_tiled_s32.restype = I
     lib.oflow_corr_pyramid_tiled_s32.argtypes = [P, P, I, I, I, I, I, PP, P]
     lib.oflow_corr_lookup_convc1_s32.restype = I
@@ -822,6 +828,23 @@ def conv_s32(x: S32Slice, cw: ConvWeights, block_n: int, act: str = "none", out_
             ),
             what,
         )
+
+
+def flow_head2(x: "S32Slice", weight: torch.Tensor, bias: torch.Tensor, coords: torch.Tensor) -> None:
+    """coords += conv3x3(x, weight, bias) for the flow head's 2-channel output conv as fp32 FMAs (oflow_flow_head2_s32;
+    update.py:36, raft.py:133), the small-grid form. x: S32Slice of C <= 256 channels; weight (2, C, 3, 3) fp32
+    contiguous; coords (B, 2, H, W) fp32 contiguous."""
+    what = "flow_head2"
+    b, h, w = x.bhw
+    if weight.dtype != torch.float32 or not weight.is_contiguous() or tuple(weight.shape) != (2, x.ng * 32, 3, 3):
+        raise RuntimeError(f"{what}: weight must be contiguous fp32 (2, {x.ng * 32}, 3, 3)")
+    if bias is None or bias.dtype != torch.float32 or tuple(bias.shape) != (2,):
+        raise RuntimeError(f"{what}: bias must be fp32 (2,)")
+    if coords.dtype != torch.float32 or not coords.is_contiguous() or tuple(coords.shape) != (b, 2, h, w):
+        raise RuntimeError(f"{what}: coords must be contiguous fp32 ({b}, 2, {h}, {w})")
+    with torch.cuda.device(coords.device), _Timed("conv3x3", coords.device):
+        _check(load().oflow_flow_head2_s32(x.ptr, x.ps, x.ng, weight.data_ptr(), bias.data_ptr(), b, h, w,
+                                           coords.data_ptr(), _stream(coords.device)), what)
 
 
 def stem_patches(img: torch.Tensor, out: torch.Tensor) -> torch.Tensor:
