@@ -19,6 +19,10 @@ from torch import Tensor
 from optical_flow import _native
 
 
+
+# output-channel block (workgroup N) per update-block conv of the split path; tools/exp/run_conv_bn_ab.py A/Bs them
+CONV_BN = {"c2": 64, "f1": 128, "f2": 64, "mo": 128, "gru": 128, "fh1": 128}
+
 class FlowHead(nn.Module):
     def __init__(self, input_dim: int = 128, hidden_dim: int = 256) -> None:
         super().__init__()
@@ -318,23 +322,23 @@ class SplitUpdate:
             side.wait_stream(main)
             with torch.cuda.stream(side):
                 _native.flow_prep(coords1, self.pm, (V(self.hx), 382), (V(self.rhx), 382))
-                conv(V(self.pm), w["f1"], 128, "relu", y0=V(self.f1))
-                conv(V(self.f1), w["f2"], 64, "relu", y0=V(self.cf, 6, 2))
+                conv(V(self.pm), w["f1"], CONV_BN["f1"], "relu", y0=V(self.f1))
+                conv(V(self.f1), w["f2"], CONV_BN["f2"], "relu", y0=V(self.cf, 6, 2))
             self._convc1(corr_in)
-            conv(V(self.c1), w["c2"], 64, "relu", y0=V(self.cf, 0, 6))
+            conv(V(self.c1), w["c2"], CONV_BN["c2"], "relu", y0=V(self.cf, 0, 6))
             main.wait_stream(side)
         else:
             _native.flow_prep(coords1, self.pm, (V(self.hx), 382), (V(self.rhx), 382))
             self._convc1(corr_in)
-            conv(V(self.c1), w["c2"], 64, "relu", y0=V(self.cf, 0, 6))
-            conv(V(self.pm), w["f1"], 128, "relu", y0=V(self.f1))
-            conv(V(self.f1), w["f2"], 64, "relu", y0=V(self.cf, 6, 2))
-        conv(V(self.cf), w["mo"], 128, "relu", y0=V(self.hx, 8, 4), y1=V(self.rhx, 8, 4))
+            conv(V(self.c1), w["c2"], CONV_BN["c2"], "relu", y0=V(self.cf, 0, 6))
+            conv(V(self.pm), w["f1"], CONV_BN["f1"], "relu", y0=V(self.f1))
+            conv(V(self.f1), w["f2"], CONV_BN["f2"], "relu", y0=V(self.cf, 6, 2))
+        conv(V(self.cf), w["mo"], CONV_BN["mo"], "relu", y0=V(self.hx, 8, 4), y1=V(self.rhx, 8, 4))
         for tag in ("1", "2"):
-            conv(V(self.hx), w["zr" + tag], 128, epilogue=1, y0=V(self.rhx, 0, 4), gru_h=self.hm, gru_z=self.z)
-            conv(V(self.rhx), w["q" + tag], 128, epilogue=2, y0=V(self.hx, 0, 4), gru_h=self.hm, gru_z=self.z)
+            conv(V(self.hx), w["zr" + tag], CONV_BN["gru"], epilogue=1, y0=V(self.rhx, 0, 4), gru_h=self.hm, gru_z=self.z)
+            conv(V(self.rhx), w["q" + tag], CONV_BN["gru"], epilogue=2, y0=V(self.hx, 0, 4), gru_h=self.hm, gru_z=self.z)
         net = V(self.hx, 0, 4)
-        conv(net, w["fh1"], 128, "relu", y0=V(self.fh))
+        conv(net, w["fh1"], CONV_BN["fh1"], "relu", y0=V(self.fh))
         if coords1.is_contiguous() and coords1.numel() // 2 < _native.FLOW_HEAD2_MAX_PIXELS:
             _native.flow_head2(V(self.fh), *w["fh2_f32"], coords1)  # coords1 += conv2(.) (raft.py:133)
         else:
