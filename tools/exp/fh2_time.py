@@ -18,12 +18,11 @@ for b in (1, 4, 8):
     wt = torch.randn(2, 256, 3, 3, device=dev) / 48
     bias = torch.randn(2, device=dev)
     coords = torch.zeros(b, 2, 55, 128, device=dev)
-    cw = N.ConvWeights(wt, bias, 16)
     ts = []
     for it in range(40):
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record()
-        N.flow_head2(N.S32Slice(xs), cw, coords)
+        N.flow_head2(N.S32Slice(xs), wt, bias, coords)
         e1.record()
         torch.cuda.synchronize()
         if it >= 5:
