@@ -256,6 +256,20 @@ int oflow_conv_s32_ex2(const void* d_x, long long x_pixel_stride, int in_groups,
                        int gru_channels, float* d_nhwc, int nhwc_pixel_stride, float* d_stats, const void* d_res,
                        long long res_pixel_stride, int res_activation, int s2d, int in_format,
                        const float* d_in_scale, const float* d_in_shift, void* stream);
+/* oflow_conv_s32_ex3: oflow_conv_s32_ex2 plus an fp32 NHWC addend d_addend[P * addend_pixel_stride + n] added to the
+ * pre-activation value after the scale and bias (GRU epilogues 1 and 2 only; 16-B aligned, addend_pixel_stride >= N,
+ * a multiple of 4; NULL = none). It carries the GRU's loop-invariant context term: x = [inp | motion] (update.py:153-154)
+ * and inp never changes across iterations (raft.py:115-118), so W_inp * inp + bias is computed once per forward and the
+ * per-iteration z / r / q convolutions (update.py:92-105) run over [h | motion | flow] only. */
+int oflow_conv_s32_ex3(const void* d_x, long long x_pixel_stride, int in_groups, const void* d_wpack, int n_pad,
+                       const float* d_wscale, const float* d_bias, int N, int B, int H, int W, int kh, int kw,
+                       int block_n, int epilogue, int activation, float out_scale, void* d_y0, long long y0_pixel_stride,
+                       void* d_y1, long long y1_pixel_stride, float* d_f32, long long f32_batch_stride,
+                       long long f32_channel_stride, int f32_accumulate, float* d_gru_h, float* d_gru_z,
+                       int gru_channels, float* d_nhwc, int nhwc_pixel_stride, float* d_stats, const void* d_res,
+                       long long res_pixel_stride, int res_activation, int s2d, int in_format,
+                       const float* d_in_scale, const float* d_in_shift, const float* d_addend,
+                       long long addend_pixel_stride, void* stream);
 int oflow_stem_patches_s32(const float* d_img, int B, int C, int H, int W, void* d_out, int out_groups, void* stream);
 int oflow_norm_stats_finalize(const float* d_partials, int B, int tiles, int n_pad, int C, double eps, float* d_alpha,
                               float* d_beta, void* stream);

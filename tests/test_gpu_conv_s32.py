@@ -157,6 +157,57 @@ def test_conv_s32_gru_epilogues():
     assert float((N.s32_to_f32(hx_s)[:, :ch].double() - hn).abs().max()) <= 2.0 ** -21
 
 
+@pytest.mark.parametrize("kh,kw", [(1, 5), (5, 1)])
+def test_conv_s32_gru_hoisted_context(kh, kw):
+    """The GRU with its loop-invariant context term hoisted (update.py:92-105, x = [inp | motion], inp constant):
+    W_inp * inp + bias once (epilogue 0, fp32 NHWC [P, 384] = z | r | q), then the z|r and q convs over
+    [h | motion | flow] only with that addend in their epilogues (oflow_conv_s32_ex3) -- against the full 384-channel
+    SepConvGRU step in float64."""
+    g = torch.Generator().manual_seed(17 + kh)
+    b, h, w, ch = 2, 9, 37, 128
+    full = torch.randn(b, 384, h, w, generator=g).to(DEV)
+    full[:, :ch] = torch.tanh(full[:, :ch])
+    full[:, ch : 2 * ch] = torch.relu(full[:, ch : 2 * ch])
+    hmf = torch.cat([full[:, :ch], full[:, 2 * ch :]], dim=1)  # [h | motion | flow]
+    hx_s = N.s32_from_f32(hmf)
+    rhx_s = hx_s.clone()
+    inp_s = N.s32_from_f32(full[:, ch : 2 * ch].contiguous())
+    hmaster = full[:, :ch].permute(0, 2, 3, 1).reshape(-1, ch).contiguous()
+    wz, wr, wq = ((torch.randn(ch, 384, kh, kw, generator=g) * 0.03).to(DEV) for _ in range(3))
+    bz, br, bq = (torch.randn(ch, generator=g).to(DEV) for _ in range(3))
+    sel = lambda wt: torch.cat([wt[:, :ch], wt[:, 2 * ch :]], dim=1)
+    cinp = N.ConvWeights(torch.cat([wz, wr, wq])[:, ch : 2 * ch], torch.cat([bz, br, bq]), 384)
+    czr = N.ConvWeights(sel(torch.cat([wz, wr])), None, 256)
+    cq = N.ConvWeights(sel(wq), None, 128)
+    gx = torch.empty(b * h * w, 384, device=DEV)
+    N.conv_s32(N.S32Slice(inp_s), cinp, 128, nhwc=gx)
+    z = torch.empty(b * h * w, ch, device=DEV)
+    N.conv_s32(N.S32Slice(hx_s), czr, 128, epilogue=1, y0=N.S32Slice(rhx_s, 0, 4), gru_h=hmaster, gru_z=z,
+               addend=gx[:, :256])
+    # float64 reference on the exact operands (hi + lo of every S32 input)
+    xr = torch.cat([N.s32_to_f32(hx_s)[:, :ch], N.s32_to_f32(inp_s), N.s32_to_f32(hx_s)[:, ch:]], dim=1).double()
+    pad = (kh // 2, kw // 2)
+    z_ref = torch.sigmoid(F.conv2d(xr, wz.double(), bz.double(), padding=pad))
+    r_ref = torch.sigmoid(F.conv2d(xr, wr.double(), br.double(), padding=pad))
+    zg = z.view(b, h, w, ch).permute(0, 3, 1, 2).double()
+    assert float((zg - z_ref).abs().max()) <= 2e-6
+    rhx = N.s32_to_f32(rhx_s).double()
+    assert float((rhx[:, :ch] - r_ref * full[:, :ch].double()).abs().max()) <= 2e-6
+    N.conv_s32(N.S32Slice(rhx_s), cq, 128, epilogue=2, y0=N.S32Slice(hx_s, 0, 4), gru_h=hmaster, gru_z=z,
+               addend=gx[:, 256:])
+    rxr = torch.cat([rhx[:, :ch], xr[:, ch:]], dim=1)
+    q_ref = torch.tanh(F.conv2d(rxr, wq.double(), bq.double(), padding=pad))
+    hn_ref = (1 - zg) * full[:, :ch].double() + zg * q_ref
+    hn = hmaster.view(b, h, w, ch).permute(0, 3, 1, 2).double()
+    assert float((hn - hn_ref).abs().max()) <= 2e-6
+    # the addend is refused outside the GRU epilogues and with misaligned rows
+    with pytest.raises(RuntimeError):
+        N.conv_s32(N.S32Slice(hx_s), czr, 128, f32=torch.empty(b, 256, h, w, device=DEV), addend=gx[:, :256])
+    with pytest.raises(RuntimeError):
+        N.conv_s32(N.S32Slice(hx_s), czr, 128, epilogue=1, y0=N.S32Slice(rhx_s, 0, 4), gru_h=hmaster, gru_z=z,
+                   addend=gx[:, 1:257])
+
+
 def test_pack_s32_and_flow_prep():
     g = torch.Generator().manual_seed(5)
     b, h, w = 2, 11, 29

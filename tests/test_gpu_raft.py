@@ -96,6 +96,25 @@ def test_pair_lanes_equal_single_lane(lookup, b):
     assert len(preds1) == len(preds2) == 3 and all(torch.equal(a, c) for a, c in zip(preds1, preds2))
 
 
+def test_pair_lanes_equal_single_lane_across_flow_head_threshold():
+    """3 Sintel-size pairs (55x128 grid: 21120 px for the batch, 7040 / 14080 per lane) straddle the flow head's
+    kernel choice (FLOW_HEAD2_MAX_PIXELS): the choice is made once per forward from the whole batch, so two lanes
+    still give the single-lane flows bit for bit."""
+    from optical_flow import _native
+
+    b = 3
+    assert b * 55 * 128 >= _native.FLOW_HEAD2_MAX_PIXELS > 2 * 55 * 128
+    img0, img1 = synthetic.synthetic_pair(b, 440, 1024, seed=9)
+    p0, p1 = img0.to(DEV), img1.to(DEV)
+    model = _model(RAFT)
+    outs = {}
+    with torch.inference_mode():
+        for lanes in (1, 2):
+            model.pair_lanes = lanes
+            outs[lanes] = model(p0, p1, iters=3, test_mode=True)
+    assert torch.equal(outs[1][0], outs[2][0]) and torch.equal(outs[1][1], outs[2][1])
+
+
 def test_fused_update_matches_module_update_block():
     """FusedUpdate (fused bias/activation/GRU kernels, merged z|r convolution, persistent [h | x] buffers) against
     the nn.Module update block on the same GPU, two steps so the carried state is checked too."""

@@ -60,6 +60,10 @@ struct ConvArgs {
   float* h;
   float* z;
   int gch;
+  // fp32 NHWC addend [P][addps] added to the pre-activation value (after scale and bias), or null: the GRU's
+  // loop-invariant context term, computed once per forward (EPI 1, 2)
+  const float* add;
+  long long addps;
   // encoder options (EPI 0)
   float* fn;               // fp32 NHWC destination [P][fnps] (pre-activation value when stats are taken) or null
   int fnps;
@@ -376,6 +380,25 @@ __global__ __launch_bounds__(64 * WM * WN, WM * WN == 8 ? 1 : 2) void conv_s32_k
 #undef OFLOW_WRITE_B
 
   // ---- epilogue: accumulators -> LDS tile [pixel][channel] ----
+  constexpr int C8 = BN / 8;
+  constexpr int KIT = (BM * C8 + NTH - 1) / NTH;  // epilogue items (pixel x 8 channels) per thread
+  // GRU addend (the hoisted context term): its loads are issued here, so they fly while the accumulators go to LDS,
+  // and it is folded into the tile (with the scale and bias) before the GRU state is prefetched -- never both sets
+  // of registers live at once
+  const bool has_add = EPI != 0 && a.add != nullptr;
+  u32x4 ad[EPI == 0 ? 1 : KIT][2];
+  if (has_add) {
+#pragma unroll
+    for (int k = 0; k < (EPI == 0 ? 0 : KIT); ++k) {
+      const int item = tid + k * NTH;
+      const int pl = item / C8, n = n0 + (item - pl * C8) * 8;
+      const int y = ty0 + pl / kTX, x = tx0 + (pl % kTX);
+      if (item >= BM * C8 || n >= a.N || y >= a.H || x >= a.W) continue;
+      const u32x4* ap = reinterpret_cast<const u32x4*>(a.add + (pix0 + (long long)y * a.W + x) * a.addps + n);
+      ad[k][0] = ap[0];
+      ad[k][1] = ap[1];
+    }
+  }
   __syncthreads();  // the tile overwrites the operand buffers: every wave is past its last LDS operand read
   float* sT = reinterpret_cast<float*>(smem);
 #pragma unroll
@@ -391,6 +414,24 @@ __global__ __launch_bounds__(64 * WM * WN, WM * WN == 8 ? 1 : 2) void conv_s32_k
       }
     }
   __syncthreads();
+  if (has_add) {
+    // pre-activation value = acc * scale + bias + addend, in place (each thread rewrites only its own items, which it
+    // alone reads below: no barrier)
+#pragma unroll
+    for (int k = 0; k < (EPI == 0 ? 0 : KIT); ++k) {
+      const int item = tid + k * NTH;
+      const int pl = item / C8, nl = (item - pl * C8) * 8, n = n0 + nl;
+      const int y = ty0 + pl / kTX, x = tx0 + (pl % kTX);
+      if (item >= BM * C8 || n >= a.N || y >= a.H || x >= a.W) continue;
+      const float* av = reinterpret_cast<const float*>(&ad[k][0]);
+      float* tp = &sT[pl * TS + nl];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float2 sb = sSB[nl + j];
+        tp[j] = (tp[j] * sb.x + sb.y) + av[j];
+      }
+    }
+  }
 
   if (a.f != nullptr) {
     // fp32 NCHW: lanes = consecutive pixels of one tile row (128-B rows of the destination)
@@ -475,8 +516,6 @@ __global__ __launch_bounds__(64 * WM * WN, WM * WN == 8 ? 1 : 2) void conv_s32_k
   // S32 / GRU consumers: one thread = one pixel x 8 consecutive channels, KIT items per thread. The GRU state operands
   // of every item (h; z) are loaded first, all in flight at once, then consumed: one memory round trip per epilogue
   // instead of one per item.
-  constexpr int C8 = BN / 8;
-  constexpr int KIT = (BM * C8 + NTH - 1) / NTH;
   u32x4 pre[EPI == 0 ? 1 : KIT][EPI == 2 ? 4 : 2];
 #pragma unroll
   for (int k = 0; k < (EPI == 0 ? 0 : KIT); ++k) {
@@ -513,10 +552,12 @@ __global__ __launch_bounds__(64 * WM * WN, WM * WN == 8 ? 1 : 2) void conv_s32_k
     const float4 t0 = *reinterpret_cast<const float4*>(&sT[pl * TS + nl]);
     const float4 t1 = *reinterpret_cast<const float4*>(&sT[pl * TS + nl + 4]);
     float v[8] = {t0.x, t0.y, t0.z, t0.w, t1.x, t1.y, t1.z, t1.w};
+    if (!has_add) {  // (with the addend the tile already holds the pre-activation value)
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const float2 sb = sSB[nl + j];
-      v[j] = v[j] * sb.x + sb.y;
+      for (int j = 0; j < 8; ++j) {
+        const float2 sb = sSB[nl + j];
+        v[j] = v[j] * sb.x + sb.y;
+      }
     }
     if constexpr (EPI == 0) {
 #pragma unroll
@@ -737,7 +778,7 @@ int build_conv_args(ConvArgs& a, const void* d_x, long long x_pixel_stride, int 
 
 using namespace oflow;
 
-extern "C" int oflow_conv_s32_ex2(const void* d_x, long long x_pixel_stride, int in_groups, const void* d_wpack,
+extern "C" int oflow_conv_s32_ex3(const void* d_x, long long x_pixel_stride, int in_groups, const void* d_wpack,
                                   int n_pad, const float* d_wscale, const float* d_bias, int N, int B, int H, int W, int kh,
                                   int kw, int block_n, int epilogue, int activation, float out_scale, void* d_y0,
                                   long long y0_pixel_stride, void* d_y1, long long y1_pixel_stride, float* d_f32,
@@ -745,7 +786,7 @@ extern "C" int oflow_conv_s32_ex2(const void* d_x, long long x_pixel_stride, int
                                   float* d_gru_h, float* d_gru_z, int gru_channels, float* d_nhwc, int nhwc_pixel_stride,
                                   float* d_stats, const void* d_res, long long res_pixel_stride, int res_activation,
                                   int s2d, int in_format, const float* d_in_scale, const float* d_in_shift,
-                                  void* stream) {
+                                  const float* d_addend, long long addend_pixel_stride, void* stream) {
   ConvArgs a;
   const int st = build_conv_args(a, d_x, x_pixel_stride, in_groups, d_wpack, n_pad, d_wscale, d_bias, N, B, H, W, kh, kw,
                                  block_n, epilogue, activation, out_scale, d_y0, y0_pixel_stride, d_y1, y1_pixel_stride,
@@ -770,7 +811,29 @@ extern "C" int oflow_conv_s32_ex2(const void* d_x, long long x_pixel_stride, int
     if (kh != 1 || kw != 1 || epilogue != 0 || block_n != 128) return OFLOW_E_MODE;
   }
   a.ain = in_format;
+  if (d_addend) {  // GRU epilogues only; 16-B aligned rows of >= N floats
+    if (epilogue == 0) return OFLOW_E_MODE;
+    if (((uintptr_t)d_addend & 15) || (addend_pixel_stride & 3) || addend_pixel_stride < N) return OFLOW_E_ALIGN;
+    a.add = d_addend;
+    a.addps = addend_pixel_stride;
+  }
   return dispatch_conv(a, kh, kw, block_n, epilogue, static_cast<hipStream_t>(stream));
+}
+
+extern "C" int oflow_conv_s32_ex2(const void* d_x, long long x_pixel_stride, int in_groups, const void* d_wpack,
+                                  int n_pad, const float* d_wscale, const float* d_bias, int N, int B, int H, int W, int kh,
+                                  int kw, int block_n, int epilogue, int activation, float out_scale, void* d_y0,
+                                  long long y0_pixel_stride, void* d_y1, long long y1_pixel_stride, float* d_f32,
+                                  long long f32_batch_stride, long long f32_channel_stride, int f32_accumulate,
+                                  float* d_gru_h, float* d_gru_z, int gru_channels, float* d_nhwc, int nhwc_pixel_stride,
+                                  float* d_stats, const void* d_res, long long res_pixel_stride, int res_activation,
+                                  int s2d, int in_format, const float* d_in_scale, const float* d_in_shift,
+                                  void* stream) {
+  return oflow_conv_s32_ex3(d_x, x_pixel_stride, in_groups, d_wpack, n_pad, d_wscale, d_bias, N, B, H, W, kh, kw,
+                            block_n, epilogue, activation, out_scale, d_y0, y0_pixel_stride, d_y1, y1_pixel_stride,
+                            d_f32, f32_batch_stride, f32_channel_stride, f32_accumulate, d_gru_h, d_gru_z, gru_channels,
+                            d_nhwc, nhwc_pixel_stride, d_stats, d_res, res_pixel_stride, res_activation, s2d, in_format,
+                            d_in_scale, d_in_shift, nullptr, 0, stream);
 }
 
 extern "C" int oflow_conv_s32_ex(const void* d_x, long long x_pixel_stride, int in_groups, const void* d_wpack,

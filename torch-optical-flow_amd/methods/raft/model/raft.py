@@ -183,7 +183,8 @@ class RAFT(nn.Module):
         for i, ((b0, b1), st) in enumerate(zip(cuts, lanes)):
             with torch.cuda.stream(st):
                 slot = 0 if i == 0 else 200 + i
-                runners.append(SplitUpdate(self.update_block, cnet_out[b0:b1], hdim, side_slot=slot, fuse_c1=self.lookup_fusion))
+                runners.append(SplitUpdate(self.update_block, cnet_out[b0:b1], hdim, side_slot=slot, fuse_c1=self.lookup_fusion,
+                                           flow_head_pixels=cnet_out.shape[0] * cnet_out.shape[2] * cnet_out.shape[3]))
         joined = self.pair_lookup == "joined" and not runners[0].fusable(corr_fn)
         hw = cnet_out.shape[2] * cnet_out.shape[3]
         if joined:

@@ -203,10 +203,14 @@ class SplitUpdate:
 
     Activations live in S32 buffers (split-fp16 NHWC by 32-channel groups, include/oflow.h), laid out so that no
     concatenation is ever copied (`update.py:93, 96, 100, 103, 127, 155`):
-      hx  = [h | inp | motion(126) | flow(2)]   (GRU input of the z, r gates)     12 groups
-      rhx = [r*h | inp | motion | flow]          (GRU input of the candidate)      12 groups
+      hx  = [h | motion(126) | flow(2)]   (GRU input of the z, r gates)     8 groups
+      rhx = [r*h | motion | flow]          (GRU input of the candidate)      8 groups
       cf  = [relu(convc2) (192) | relu(convf2) (64)]  (input of the motion conv)  8 groups
     h is also kept in fp32 ([P, 128]) so that the blend h = (1-z)h + zq (`update.py:97`) runs in fp32.
+    The GRU input is x = [inp | motion] (`update.py:153-154`) and inp, cnet's context half (`raft.py:115-118`), never
+    changes across iterations: its share of every z / r / q pre-activation, W_inp * inp + bias, is computed once per
+    forward for both passes (fp32 [P, 384] per pass: z | r | q) and added in the GRU epilogues, so the per-iteration
+    convolutions contract [h | motion | flow] only (K: 12 -> 8 groups).
     Per iteration: the lookup fused into convc1 (oflow_corr_lookup_convc1_s32: the lookup volume is never written;
     otherwise lookup -> fp32 NHWC rows -> convc1), flow_prep -> flow channels + convf1's 7x7 patch matrix, then
     convc2, convf1 (1x1 over the patches), convf2, conv (-> hx, rhx), [z|r] (-> z, r*h -> rhx),
@@ -215,7 +219,7 @@ class SplitUpdate:
     """
 
     def __init__(self, block: BasicUpdateBlock, cnet_out: Tensor, hdim: int, side_slot: int = 0,
-                 fuse_c1: bool = True) -> None:
+                 fuse_c1: bool = True, flow_head_pixels: Optional[int] = None) -> None:
         b, c, h, w = cnet_out.shape
         enc, gru = block.encoder, block.gru
         cdim = c - hdim
@@ -223,9 +227,13 @@ class SplitUpdate:
             raise RuntimeError("SplitUpdate: supports the RAFT (large) update block only")
         dev = cnet_out.device
         self.block, self.shape = block, (b, h, w)
+        # the flow head's output conv: the fp32-FMA kernel or the split conv (not bit-identical to each other), chosen
+        # from the pixel count of the WHOLE forward's batch so that pair lanes give the single-lane results bit for bit
+        px = b * h * w if flow_head_pixels is None else int(flow_head_pixels)
+        self.flow_head_fma = px < _native.FLOW_HEAD2_MAX_PIXELS
         S = _native.s32_empty
-        self.hx = S(b, h, w, 12, dev)
-        self.rhx = S(b, h, w, 12, dev)
+        self.hx = S(b, h, w, 8, dev)
+        self.rhx = S(b, h, w, 8, dev)
         levels, radius = block.corr_levels, block.corr_radius
         self.corr_ch = levels * (2 * radius + 1) ** 2  # convc1's input: fp32 NHWC lookup rows in the reference order
         self.corr_f32 = None  # [B*H*W, corr_ch], allocated on first use
@@ -238,8 +246,15 @@ class SplitUpdate:
         self.z = torch.empty_like(self.hm)
         V = _native.S32Slice
         _native.pack_s32(cnet_out[:, :hdim], "tanh", V(self.hx, 0, 4), nhwc=self.hm)  # raft.py:117
-        _native.pack_s32(cnet_out[:, hdim:], "relu", V(self.hx, 4, 4), V(self.rhx, 4, 4))  # raft.py:118
+        inp = S(b, h, w, 4, dev)
+        _native.pack_s32(cnet_out[:, hdim:], "relu", V(inp))  # raft.py:118
         self.w = self._weights(block)
+        # the GRU's loop-invariant context term of both passes: [z | r | q] pre-activations of inp + bias
+        self.gx = []
+        for tag in ("1", "2"):
+            gx = torch.empty((b * h * w, 3 * hdim), device=dev, dtype=torch.float32)
+            _native.conv_s32(V(inp), self.w["inp" + tag], 128, nhwc=gx)
+            self.gx.append(gx)
         self.fuse_c1 = fuse_c1 and "c1L" in self.w
         # side stream for the motion encoder's flow branch (one per device, reused across forwards)
         self.streams = getattr(block, "split_streams", True)
@@ -269,9 +284,14 @@ class SplitUpdate:
         if block.corr_radius in (3, 4):  # the lookup fused into convc1 (corr_convc1.hip): weights regrouped per level
             w["c1L"] = _native.convc1_level_weights(enc.convc1, block.corr_levels, block.corr_radius)
         for tag in ("1", "2"):
+            # GRU input channels (update.py:93-103): [h 0..127 | inp 128..255 | motion 256..381 | flow 382, 383]; the
+            # per-iteration convs take [h | motion | flow] (no bias), the hoisted one inp with the z | r | q biases
             cz, cr, cq = (getattr(gru, f"conv{g}{tag}") for g in "zrq")
-            w["zr" + tag] = CW(torch.cat([cz.weight, cr.weight]), torch.cat([cz.bias, cr.bias]), 256)
-            w["q" + tag] = CW(cq.weight, cq.bias, 128)
+            hmf = lambda wt: torch.cat([wt[:, :128], wt[:, 256:]], dim=1)
+            w["zr" + tag] = CW(hmf(torch.cat([cz.weight, cr.weight])), None, 256)
+            w["q" + tag] = CW(hmf(cq.weight), None, 128)
+            w["inp" + tag] = CW(torch.cat([cz.weight, cr.weight, cq.weight])[:, 128:256],
+                                torch.cat([cz.bias, cr.bias, cq.bias]), 384)
         block.__dict__["_split_weights"] = (key, w)
         return w
 
@@ -321,25 +341,27 @@ class SplitUpdate:
         if side is not None:
             side.wait_stream(main)
             with torch.cuda.stream(side):
-                _native.flow_prep(coords1, self.pm, (V(self.hx), 382), (V(self.rhx), 382))
+                _native.flow_prep(coords1, self.pm, (V(self.hx), 254), (V(self.rhx), 254))
                 conv(V(self.pm), w["f1"], CONV_BN["f1"], "relu", y0=V(self.f1))
                 conv(V(self.f1), w["f2"], CONV_BN["f2"], "relu", y0=V(self.cf, 6, 2))
             self._convc1(corr_in)
             conv(V(self.c1), w["c2"], CONV_BN["c2"], "relu", y0=V(self.cf, 0, 6))
             main.wait_stream(side)
         else:
-            _native.flow_prep(coords1, self.pm, (V(self.hx), 382), (V(self.rhx), 382))
+            _native.flow_prep(coords1, self.pm, (V(self.hx), 254), (V(self.rhx), 254))
             self._convc1(corr_in)
             conv(V(self.c1), w["c2"], CONV_BN["c2"], "relu", y0=V(self.cf, 0, 6))
             conv(V(self.pm), w["f1"], CONV_BN["f1"], "relu", y0=V(self.f1))
             conv(V(self.f1), w["f2"], CONV_BN["f2"], "relu", y0=V(self.cf, 6, 2))
-        conv(V(self.cf), w["mo"], CONV_BN["mo"], "relu", y0=V(self.hx, 8, 4), y1=V(self.rhx, 8, 4))
-        for tag in ("1", "2"):
-            conv(V(self.hx), w["zr" + tag], CONV_BN["gru"], epilogue=1, y0=V(self.rhx, 0, 4), gru_h=self.hm, gru_z=self.z)
-            conv(V(self.rhx), w["q" + tag], CONV_BN["gru"], epilogue=2, y0=V(self.hx, 0, 4), gru_h=self.hm, gru_z=self.z)
+        conv(V(self.cf), w["mo"], CONV_BN["mo"], "relu", y0=V(self.hx, 4, 4), y1=V(self.rhx, 4, 4))
+        for tag, gx in zip(("1", "2"), self.gx):
+            conv(V(self.hx), w["zr" + tag], CONV_BN["gru"], epilogue=1, y0=V(self.rhx, 0, 4), gru_h=self.hm, gru_z=self.z,
+                 addend=gx[:, :256])
+            conv(V(self.rhx), w["q" + tag], CONV_BN["gru"], epilogue=2, y0=V(self.hx, 0, 4), gru_h=self.hm, gru_z=self.z,
+                 addend=gx[:, 256:])
         net = V(self.hx, 0, 4)
         conv(net, w["fh1"], CONV_BN["fh1"], "relu", y0=V(self.fh))
-        if coords1.is_contiguous() and coords1.numel() // 2 < _native.FLOW_HEAD2_MAX_PIXELS:
+        if self.flow_head_fma and coords1.is_contiguous():
             _native.flow_head2(V(self.fh), *w["fh2_f32"], coords1)  # coords1 += conv2(.) (raft.py:133)
         else:
             conv(V(self.fh), w["fh2"], 32, f32=coords1, f32_accumulate=True)

@@ -67,6 +67,7 @@ SYMBOLS = (
     "oflow_corr_lookup_convc1_s32",
     "oflow_corr_pyramid_tiled_s32",
     "oflow_flow_head2_s32",
+    "oflow_conv_s32_ex3",
 )
 
 _lib = None
@@ -175,6 +176,8 @@ def load() -> ctypes.CDLL:
     lib.oflow_corr_lookup_otf_f16.argtypes = [P, PP, IP, IP, I, P, I, I, I, I, I, P, P]
     lib.oflow_conv_s32_ex2.restype = I
     lib.oflow_conv_s32_ex2.argtypes = list(lib.oflow_conv_s32_ex.argtypes[:-1]) + [I, P, P, P]
+    lib.oflow_conv_s32_ex3.restype = I
+    lib.oflow_conv_s32_ex3.argtypes = list(lib.oflow_conv_s32_ex2.argtypes[:-1]) + [P, L, P]
     lib.oflow_corr_lookup_backward_f32.restype = I
     lib.oflow_corr_lookup_backward_f32.argtypes = [P, P, I, I, I, I, PP, IP, IP, I, P]
     lib.oflow_corr_pyramid_grad_combine_f32.restype = I
@@ -773,11 +776,13 @@ def conv_tiles(h: int, w: int) -> int:
 
 def conv_s32(x: S32Slice, cw: ConvWeights, block_n: int, act: str = "none", out_scale: float = 1.0, y0=None, y1=None,
              f32=None, f32_accumulate: bool = False, epilogue: int = 0, gru_h=None, gru_z=None, nhwc=None, stats=None,
-             res=None, res_act: str = "none", s2d: bool = False) -> None:
-    """Split-fp16 convolution (oflow_conv_s32_ex2). x: input S32Slice with cw.kg groups, or NhwcNormIn (3x3 only). y0/y1: S32Slice destinations
+             res=None, res_act: str = "none", s2d: bool = False, addend=None) -> None:
+    """Split-fp16 convolution (oflow_conv_s32_ex3). x: input S32Slice with cw.kg groups, or NhwcNormIn (3x3 only). y0/y1: S32Slice destinations
     (s2d: space-to-depth layout, half the spatial size). f32: (B, N', H, W) fp32 NCHW destination. nhwc: [P, N]
     fp32 destination. stats: instance-norm partials [B, conv_tiles(H, W), n_pad, 3]. res: S32Slice residual added
-    after the activation, then res_act. epilogue 1/2: GRU gates / candidate with gru_h, gru_z ([P, CH] fp32)."""
+    after the activation, then res_act. epilogue 1/2: GRU gates / candidate with gru_h, gru_z ([P, CH] fp32);
+    addend: fp32 [P, >= N] (row stride a multiple of 4, 16-B aligned) added before the gate activations (the GRU's
+    hoisted context term)."""
     what = "conv_s32"
     if CHECK_RANGE:
         _range_check(x, f"{what} {cw.kh}x{cw.kw}")
@@ -811,10 +816,17 @@ def conv_s32(x: S32Slice, cw: ConvWeights, block_n: int, act: str = "none", out_
             if tt is None or tt.dtype != torch.float32 or not tt.is_contiguous() or tt.numel() != b * h * w * gch:
                 raise RuntimeError(f"{what}: GRU state tensors must be contiguous fp32 [P, {gch}]")
         gh, gz = gru_h.data_ptr(), gru_z.data_ptr()
+    ap, aps = 0, 0
+    if addend is not None:
+        if (not epilogue or addend.dtype != torch.float32 or addend.dim() != 2 or addend.stride(1) != 1
+                or addend.shape[0] != b * h * w or addend.shape[1] < cw.n or addend.stride(0) % 4
+                or addend.data_ptr() % 16 or addend.device != x.device):
+            raise RuntimeError(f"{what}: addend must be a GRU-epilogue fp32 [P, >= {cw.n}] view with 16-B aligned rows")
+        ap, aps = addend.data_ptr(), addend.stride(0)
     dev = x.device
     with torch.cuda.device(dev), _Timed(f"conv{cw.kh}x{cw.kw}", dev):
         _check(
-            load().oflow_conv_s32_ex2(
+            load().oflow_conv_s32_ex3(
                 x.ptr, x.ps, cw.kg, cw.pack.data_ptr(), cw.n_pad, cw.wscale.data_ptr(),
                 cw.bias.data_ptr() if cw.bias is not None else None, cw.n, b, h, w, cw.kh, cw.kw, int(block_n),
                 int(epilogue), ACT[act], float(out_scale), y0.ptr if y0 is not None else None, y0.ps if y0 is not None else 0,
@@ -824,7 +836,7 @@ def conv_s32(x: S32Slice, cw: ConvWeights, block_n: int, act: str = "none", out_
                 stats.data_ptr() if stats is not None else None,
                 res.ptr if res is not None else None, res.ps if res is not None else 0, ACT[res_act], int(bool(s2d)),
                 in_format, x.scale.data_ptr() if nin else None, x.shift.data_ptr() if nin else None,
-                _stream(dev),
+                ap or None, aps, _stream(dev),
             ),
             what,
         )
