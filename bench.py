@@ -59,6 +59,44 @@ def lookup_bytes(batch: int, dims, radius: int = 4, s_corr: int = 4) -> int:
     return batch * n * per_q
 
 
+def warp_leg(dev, reps: int = 20):
+    """The flow-warp operator (`optical_flow.warp`, reference operator.py:8-33) at SURVEY §8(d)'s warp workload: frame
+    (8, 3, 436, 1024), flow = normalize(N(0, 8^2) px) per pixel (seeded), default modes (bilinear, border,
+    align_corners=False); timed after the timed region with HIP events on the launch stream (two frame/flow pairs
+    alternating so that no launch finds its inputs in the Infinity Cache). Algorithmic bytes (2C + 2) * 4 per pixel
+    (frame read + flow read + output write)."""
+    import optical_flow
+    from model import synthetic
+
+    b, c, h, w = 8, 3, 436, 1024
+    pairs = []
+    for k in range(2):
+        frame, _ = synthetic.synthetic_pair(b, h, w, seed=1 + k)
+        flow = optical_flow.normalize(torch.from_numpy(synthetic.hash_normal(5 + k, (b, 2, h, w), 8.0)))
+        pairs.append((frame.to(dev), flow.to(dev)))
+    stream = torch.cuda.current_stream(dev)
+    with torch.inference_mode():
+        for fr, fl in pairs:
+            optical_flow.warp(fr, fl)
+        torch.cuda.synchronize(dev)
+        evs = []
+        for i in range(reps):
+            fr, fl = pairs[i % 2]
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(stream)
+            optical_flow.warp(fr, fl)
+            e1.record(stream)
+            evs.append((e0, e1))
+        torch.cuda.synchronize(dev)
+    ms = mean_ms(evs)
+    nbytes = (2 * c + 2) * 4 * b * h * w
+    ach = nbytes / (ms * 1e-3) / 1e9
+    return {"note": "optical_flow.warp (HIP grid_warp, bilinear/border/align_corners=False) on frame (8, 3, 436, 1024), "
+                    "flow normalize(N(0, 8^2) px), timed after the timed region; not part of the RAFT step",
+            "bound": "hbm", "launch_ms": round(ms, 5), "launches": reps, "algorithmic_bytes_per_launch": nbytes,
+            "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4)}
+
+
 def pyramid_cost(batch: int, dims, c: int = 256):
     h0, w0 = dims[0]
     n = h0 * w0
@@ -169,17 +207,30 @@ def _cpu_model() -> str:
     return "unknown"
 
 
+def _cgroup_cpus():
+    """CPUs this process's cgroup may use (cgroup v2 cpu.max quota / period, rounded up), or None without a quota."""
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()[:2]
+        if q == "max":
+            return None
+        return max(1, -(-int(q) // int(per)))
+    except (OSError, ValueError):
+        return None
+
+
 def cpu_baseline(h: int, w: int, iters: int, pairs: int):
     """The oracle RAFT (PyTorch-CPU fp32 restatement of the reference, validated against its goldens) on this host:
-    torch threads = the CPUs this process may run on (sched_getaffinity), capped by OMP_NUM_THREADS where the box
-    sets the process's CPU share; 1 warm-up pair, then ``pairs`` pairs as one batch (configs #1 and
-    #3 / one 8-pair shard of #4 -- the workload's own per-GPU batch)."""
+    torch threads = the CPUs this process may run on (len(sched_getaffinity)), limited only by a cgroup
+    CPU quota when one is set (more threads than the quota's CPUs just time-slice); 1 warm-up pair, then ``pairs``
+    pairs as one batch (configs #1 and #3 / one 8-pair shard of #4 -- the workload's own per-GPU
+    batch)."""
     from model import synthetic
     from oracle import raft as oraft
 
     affinity = len(os.sched_getaffinity(0))
-    cap = int(os.environ.get("OMP_NUM_THREADS", affinity) or affinity)
-    threads = max(1, min(affinity, cap))
+    quota = _cgroup_cpus()
+    threads = max(1, min(affinity, quota) if quota else affinity)
     prev = torch.get_num_threads()
     torch.set_num_threads(threads)
     try:
@@ -200,11 +251,12 @@ def cpu_baseline(h: int, w: int, iters: int, pairs: int):
         "unit": "image-pairs/s",
         "cores": threads,
         "affinity_cpus": affinity,
+        "cgroup_cpu_quota": quota,
         "cpu_model": _cpu_model(),
         "kind": "port",
         "sample": f"oracle RAFT (PyTorch-CPU fp32 restatement of the reference), {pairs} pair(s) {h}x{w} padded as one "
         f"batch, {iters} iters, test_mode, after a 1-pair warm-up: {sec:.2f} s ({sec / pairs:.2f} s/pair); "
-        f"torch threads={threads} of {affinity} CPUs in the affinity mask",
+        f"torch threads={threads} of {affinity} CPUs in the affinity mask (cgroup CPU quota: {quota or 'none'})",
     }
 
 
@@ -356,9 +408,10 @@ def main() -> int:
     # the RAFT forward builds its pyramid from split-fp16 features (split encoders + CorrBlock); the "corr" workload
     # calls the CorrBlock API (fp32 MFMA pyramid)
     split_pyr = model.split_corr and args.update_impl == "split" and args.workload != "corr" and not alt
-    api_lookup = None
+    api_lookup = warp = None
     if rank == 0 and rec is not None and args.workload in ("sintel", "kitti") and not alt:
         api_lookup = lookup_api_leg(ppg, dims, out[0], dev)
+        warp = warp_leg(dev)
 
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
@@ -442,6 +495,8 @@ def main() -> int:
             line["kernels"]["corr_pyramid"] = pyramid_entry(pk, ppg, dims, split=split_pyr)
         if api_lookup is not None:
             line["kernels"]["corr_lookup_api"] = api_lookup
+        if warp is not None:
+            line["kernels"]["warp"] = warp
     elif rec and rec.get("corr_lookup"):
         lk = rec.get("corr_lookup", [])
         pk = rec.get("corr_pyramid", [])
@@ -467,7 +522,8 @@ def main() -> int:
             line["kernels"] = {"corr_pyramid": pyramid_entry(pk, ppg, dims, split=split_pyr)}
     if epe is not None:
         line["epe_vs_reference"] = {k: (round(v, 8) if isinstance(v, float) else v) for k, v in epe.items()}
-    if rank == 0 and world == 1 and not args.no_cpu_baseline and args.workload in ("sintel", "kitti"):
+    if rank == 0 and not args.no_cpu_baseline and args.workload in ("sintel", "kitti"):
+        # after every rank's timing (the all-reduce above): the oracle on rank 0's host cores, a bounded sample
         line["cpu_baseline"] = cpu_baseline(h, w, iters, ppg)
     if rank == 0:
         print(json.dumps(line), flush=True)

@@ -208,8 +208,11 @@ int oflow_corr_lookup_tiled_nhwc_f32(const float* const* d_levels, const int* le
  * y = relu(convc1(corr_fn(coords))) (256 channels: d_y + P * y_pixel_stride, 8 groups), the lookup volume never
  * written. Replaces raft.py:128 (corr.py:56-77) + update.py:120-121 (`F.relu(self.convc1(corr))`) in the forward.
  * Weights: oflow_conv_s32's packing (1x1, n_pad 256) of convc1 with its input channels regrouped per level -- level l's
- * tap k at channel l*G*32 + k, G = ceil((2r+1)^2/32), zeros elsewhere (num_levels*G groups); d_wscale [256], d_bias [256]
- * or NULL. radius 3 or 4 (else OFLOW_E_RADIUS), y_pixel_stride % 128 == 0. */
+ * tap k at channel l*G*32 + k, G = ceil((2r+1)^2/32), zeros elsewhere (num_levels*G k32 groups) -- stored
+ * fragment-major: [group][wave 4][n tile 2][sub 2][hi, lo][lane 64][8 fp16], where lane = hh*32 + r holds output channel
+ * wave*64 + ntile*32 + r, inputs k = 16*sub + 8*hh .. +7 of the group (the same bytes as the conv packing
+ * [group][256][hi 32 | lo 32], permuted); d_wscale [256], d_bias [256] or NULL. radius 3 or 4 (else OFLOW_E_RADIUS),
+ * y_pixel_stride % 128 == 0. */
 int oflow_corr_lookup_convc1_s32(const float* const* d_levels, const int* level_h, const int* level_w, int num_levels,
                                  const float* d_coords, int B, int H, int W, int radius, const void* d_wpack,
                                  const float* d_wscale, const float* d_bias, void* d_y, long long y_pixel_stride,

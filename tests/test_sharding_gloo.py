@@ -116,3 +116,24 @@ def test_shard_bounds_cover_batch():
             assert spans[0][0] == 0 and spans[-1][1] == b
             assert all(spans[i][1] == spans[i + 1][0] for i in range(w - 1))
             assert max(s1 - s0 for s0, s1 in spans) - min(s1 - s0 for s0, s1 in spans) <= 1
+
+
+def _shape_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        img = torch.zeros(3, 3, 16, 24)
+        try:
+            scatter_pairs(img, img, torch.device("cpu"), shape=(4, 3, 16, 24))
+            q.put((rank, False))
+        except ValueError:
+            q.put((rank, True))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_scatter_refuses_a_shape_that_disagrees_with_the_batch():
+    """A caller-given global shape is checked against the source batch on the source rank (host-only, before any
+    collective): a mismatch raises instead of mis-sizing the scatter."""
+    res = _run(_shape_worker, 1)
+    assert res == [(0, True)]

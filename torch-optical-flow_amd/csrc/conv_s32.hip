@@ -540,6 +540,14 @@ __global__ __launch_bounds__(64 * WM * WN, WM * WN == 8 ? 1 : 2) void conv_s32_k
     }
   }
   constexpr int UNR = EPI == 0 ? 1 : KIT;  // GRU: unrolled (pre[k] in registers); EPI 0: a plain loop
+  // where every item of a thread has the same channel octet (NTH a multiple of BN / 8), its (scale, bias) pairs are
+  // read once: in the plain loop each item would otherwise wait on 8 dependent LDS round trips
+  constexpr bool FIXED_OCT = NTH % C8 == 0;
+  float2 sbv[8];
+  if constexpr (FIXED_OCT) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) sbv[j] = sSB[(tid % C8) * 8 + j];
+  }
 #pragma unroll UNR
   for (int k = 0; k < KIT; ++k) {
     const int item = tid + k * NTH;
@@ -555,7 +563,7 @@ __global__ __launch_bounds__(64 * WM * WN, WM * WN == 8 ? 1 : 2) void conv_s32_k
     if (!has_add) {  // (with the addend the tile already holds the pre-activation value)
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
-        const float2 sb = sSB[nl + j];
+        const float2 sb = FIXED_OCT ? sbv[j] : sSB[nl + j];
         v[j] = v[j] * sb.x + sb.y;
       }
     }

@@ -2,24 +2,21 @@
 //
 // Replaces, in the RAFT forward, `corr = corr_fn(coords1)` (methods/raft/model/raft.py:128 -> corr.py:56-77) followed
 // by `F.relu(self.convc1(corr))` (update.py:120-121, a 1x1 conv L*(2r+1)^2 -> 256): the (B, 324, H, W) lookup volume
-// never reaches HBM. Per workgroup of 64 query pixels (4 waves; two workgroups per CU, so one's gather / tap phases
-// overlap the other's MFMAs), level by level:
-//   1. the (2r+2)^2 window patches of the level, gathered from the tiled pyramid (4x8 tiles = 128-B lines, the
-//      layout corr_lookup.hip reads; 25 scalar loads per thread, issued during the previous level's last MFMAs), are
-//      written to LDS (odd per-query stride);
-//   2. the (2r+1)^2 bilinear taps of each query (bilinear4: the lookup kernels' arithmetic, bit for bit) become the
-//      level's split-fp16 A operand in LDS: [k32 group][pixel][hi 32 | lo 32], 16-B slots XOR-swizzled, one thread per
-//      (pixel, 8-tap slot) writing whole 16-B slots; taps past (2r+1)^2 in the level's last group stay zero;
-//   3. each wave (64 pixels x 64 output channels) runs the level's G k32 groups as split-fp16 products on
-//      v_mfma_f32_32x32x16_f16 (hi*lo + lo*hi + hi*hi, fp32 accumulate: conv_s32.hip's arithmetic); the weights
-//      stream one k32 group (256 channels x 128 B) at a time through LDS over the dead patches, register-staged one
-//      group ahead.
-// Epilogue: accumulators -> LDS [pixel][channel] fp32 -> per-channel weight scale, bias, ReLU -> S32 store of the 256
-// output channels (convc2's input).
+// never reaches HBM. A workgroup (4 waves, two workgroups per CU) owns 64 query pixels and all 256 output channels and
+// runs the levels as a pipeline (details at the kernel): level l+1's window gathers fly while level l's bilinear taps
+// (bilinear4: the lookup kernels' arithmetic, bit for bit) become the split-fp16 A operand in LDS and its k32 groups
+// run on v_mfma_f32_32x32x16_f16 (hi*lo + lo*hi + hi*hi, fp32 accumulate: conv_s32.hip's arithmetic), with the weights
+// streamed from L2 straight into the MFMA operand registers. Epilogue: accumulators -> LDS [pixel][channel] fp32 ->
+// per-channel weight scale, bias, ReLU -> S32 store of the 256 output channels (convc2's input).
 //
-// Weights: oflow_conv_s32's packing of convc1 with its input channels regrouped per level: level l's tap k at packed
-// channel l*G*32 + k (G = ceil((2r+1)^2 / 32)); the other channels are zero. Radius 3 (G = 2) and 4 (G = 3).
-// LDS: A G*8 KB + weights/patches 32 KB, epilogue tile overlay 66.5 KB, + 5.5 KB (two workgroups per CU).
+// Weights (include/oflow.h): oflow_conv_s32's packing of convc1 with its input channels regrouped per level (level l's
+// tap k at packed channel l*G*32 + k, G = ceil((2r+1)^2 / 32), zeros elsewhere; radius 3: G = 2, radius 4: G = 3),
+// stored fragment-major: [k32 group][wave 4][n tile 2][sub 2][hi, lo][lane 64][16 B], lane (r, hh) of wave w and
+// n tile nt holding channel w*64 + nt*32 + r, k = 16*sub + 8*hh .. +7 -- the MFMA's B fragment, so that one wave
+// instruction loads 1 KB contiguous.
+// LDS: patches 44.3 KB + A G*8 KB (epilogue tile overlay 66.5 KB) + 5.5 KB: two workgroups per CU.
+#include <type_traits>
+
 #include "oflow_internal.h"
 
 namespace oflow {
@@ -45,43 +42,100 @@ struct C1Args {
   const float* coords;  // (B, 2, N)
   int N;                // query pixels per batch element
   int total;            // B * N
-  const uint8_t* w;     // packed weights [nlev * G][256][hi | lo]
+  const uint8_t* wf;    // weights, fragment-major [nlev * G][4][2][2][2][64][16 B]
   const float* wsc;     // [256] inverse weight scale
   const float* bias;    // [256] or null
   uint8_t* y;           // S32 destination (8 groups of one pixel from y + P * yps)
   long long yps;
+  unsigned long long* stamps;  // diagnostics only (experiment hook): per workgroup 16 clock stamps, or null
 };
 
+// exact n / D for 0 <= n < LIM as (n * M) >> 16 with M = ceil(65536 / D) (checked at compile time)
+constexpr unsigned magic16(unsigned d) { return (65536u + d - 1) / d; }
+constexpr bool magic16_ok(unsigned d, unsigned lim) {
+  for (unsigned n = 0; n < lim; ++n)
+    if (((n * magic16(d)) >> 16) != n / d) return false;
+  return true;
+}
+
+// Per workgroup (64 queries, 4 waves; wave w = output channels 64w..64w+63), level by level:
+//   * gathers: a window row of PK cells starting at x0 lies inside NCH 16-B aligned chunks from xa = x0 & ~3 (a chunk
+//     never crosses a 4x8 tile: tile rows are 32 B), one buffer_load_dwordx4 per chunk; per-(query, level) window
+//     origin and row / column validity masks come from LDS (decoded two levels ahead), offsets are branch-free (a chunk
+//     not needed loads the workgroup's first 16 B);
+//   * patches in LDS: row u of query q at sP[q*QS + u*RW], the window's cells at +3 .. +3+PK-1; a chunk's 4 floats go
+//     to +3 + 4k + e - dx (dx = x0 - xa), the ones outside the window into the row's slack (RW >= 4*NCH: never another
+//     row's cells); cells outside the level (zero padding, Q4) are written as 0 from the masks;
+//   * level l+1's gathers are issued right after level l's patches are in LDS, so they fly during level l's taps and
+//     MFMAs;
+//   * B (weights, fragment-major: one wave instruction = 1 KB contiguous, L2-resident) goes straight into the MFMA
+//     operand registers through a 2-deep ring of k32 groups, each group's load issued right after the MFMAs of the
+//     group two before it. Vector-memory loads retire in issue order, so only a group whose load follows the next
+//     level's gathers waits for them (G = 3: the level's last group).
+// Taps, split and MFMA order are those of the round-2 kernel (LDS-staged weights, dword gathers; git history and
+// tools/build_rev.sh for A/B): the output is bit for bit the same.
 template <int R>
 __global__ __launch_bounds__(kNT, 2) void corr_convc1_kernel(C1Args a) {
-  constexpr int PK = 2 * R + 2, K = 2 * R + 1, KK = K * K, PS = PK * PK, QS = PS + 1;
-  constexpr int G = (KK + 31) / 32;      // k32 groups per level
-  constexpr int NSLOT = (KK + 7) / 8;    // 8-tap slots that hold taps
+  constexpr int PK = 2 * R + 2, K = 2 * R + 1, KK = K * K;
+  constexpr int NCH = (PK + 6) / 4;                          // chunks per window row (dx <= 3)
+  constexpr int RW = ((4 * NCH > PK + 3) ? 4 * NCH : PK + 3) | 1;  // LDS row pitch (floats; odd: spreads the
+                                                                    // chunk writes of consecutive rows over banks)
+  constexpr int QS = ((PK * RW + 3) | 1);                    // per-query pitch: odd -> conflict-free tap reads
+  constexpr int G = (KK + 31) / 32;
+  constexpr int NSLOT = (KK + 7) / 8;
   constexpr int A_BYTES = G * kQM * 128;
-  constexpr int B_BYTES = kN * 128;      // one k32 weight group
   constexpr int P_BYTES = kQM * QS * 4;
-  constexpr int TS = kN + 4;             // epilogue tile row (floats)
+  constexpr int TS = kN + 4;
   constexpr int EPI_BYTES = kQM * TS * 4;
-  constexpr int MAIN = A_BYTES + B_BYTES;
+  constexpr int MAIN = A_BYTES + P_BYTES;
   constexpr int LDS_BYTES = MAIN > EPI_BYTES ? MAIN : EPI_BYTES;
-  constexpr int GI = (kQM * PS + kNT - 1) / kNT;  // gather items per thread
-  constexpr int BI = kN * 128 / (16 * kNT);        // 16-B weight chunks per thread and group
-  static_assert(P_BYTES <= B_BYTES, "patches alias the weight buffer");
-  static_assert(kN * 128 % (16 * kNT) == 0, "weight chunks");
+  constexpr int CITEMS = kQM * PK * NCH;                     // chunk items per level
+  constexpr int NI = (CITEMS + kNT - 1) / kNT;
+  constexpr int NS = 4;                                      // decode slots (level & 3)
+  static_assert(4 * NCH <= 16 && PK <= 16, "mask widths");
   __shared__ __attribute__((aligned(16))) uint8_t smem[LDS_BYTES];
-  __shared__ float2 sSB[kN];      // per channel (inverse weight scale, bias) for the epilogue
-  __shared__ float2 sC[kQM];      // the queries' coordinates
-  __shared__ int2 sO[2][kQM];     // per level parity: window origin (x, y)
-  __shared__ float4 sW[2][kQM];   // bilinear weights (nw, ne, sw, se)
+  __shared__ float2 sSB[kN];
+  __shared__ float2 sC[kQM];
+  __shared__ int4 sO[NS][kQM];    // window origin x0, y0, masks (x: bits 0-15, y: bits 16-31), dx
+  __shared__ float4 sW[NS][kQM];  // bilinear weights (nw, ne, sw, se)
   uint8_t* sA = smem;
-  uint8_t* sB = smem + A_BYTES;
-  float* sP = reinterpret_cast<float*>(sB);
+  float* sP = reinterpret_cast<float*>(smem + A_BYTES);
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wn = wave;
   const int r = lane & 31, hh = lane >> 5;
   const int q0 = blockIdx.x * kQM;
   const int nq = min(kQM, a.total - q0);
+  int nst = 0;
+  auto stamp = [&]() {  // diagnostics (experiment hook): per-workgroup clock stamps
+    if (a.stamps != nullptr) {
+      if (tid == 0) a.stamps[(size_t)blockIdx.x * 16 + nst] = __builtin_amdgcn_s_memtime();
+      ++nst;
+    }
+  };
+  stamp();
+  auto level = [&](int l, int& Hl, int& Wl, int& WB, int& LF, const float*& base) {
+    Hl = a.Hl[0]; Wl = a.Wl[0]; WB = a.WB[0]; LF = a.LF[0]; base = a.lv[0];
+#pragma unroll
+    for (int j = 1; j < OFLOW_MAX_LEVELS; ++j)
+      if (j == l) { Hl = a.Hl[j]; Wl = a.Wl[j]; WB = a.WB[j]; LF = a.LF[j]; base = a.lv[j]; }
+  };
+  // window of query tid at level l -> sO / sW[l & 3] (threads < kQM)
+  auto decode = [&](int l, float cx, float cy) {
+    int Hl, Wl, WB, LF;
+    const float* base;
+    level(l, Hl, Wl, WB, LF, base);
+    int xs, ys;
+    float4 w4;
+    window_origin(cx, cy, 1.0f / static_cast<float>(1 << l), R, xs, ys, w4);  // 1/2^l exact (corr.py:68)
+    const int dx = xs & 3, xa = xs - dx;
+    const int xl = max(0, -xa), xh = min(4 * NCH, Wl - xa);
+    const int yl = max(0, -ys), yh = min(PK, Hl - ys);
+    const unsigned xm = xh > xl ? (((1u << (xh - xl)) - 1u) << xl) : 0u;
+    const unsigned ym = yh > yl ? (((1u << (yh - yl)) - 1u) << yl) : 0u;
+    sO[l & (NS - 1)][tid] = make_int4(xs, ys, static_cast<int>(xm | (ym << 16)), dx);
+    sW[l & (NS - 1)][tid] = w4;
+  };
 
   for (int c = tid; c < kN; c += kNT) sSB[c] = make_float2(a.wsc[c], a.bias ? a.bias[c] : 0.f);
   if (tid < kQM) {
@@ -92,75 +146,66 @@ __global__ __launch_bounds__(kNT, 2) void corr_convc1_kernel(C1Args a) {
       c = make_float2(a.coords[(size_t)(2 * b) * a.N + pix], a.coords[(size_t)(2 * b + 1) * a.N + pix]);
     }
     sC[tid] = c;
+    decode(0, c.x, c.y);
+    if (a.nlev > 1) decode(1, c.x, c.y);
   }
-  // window origin + bilinear weights of each query at level l -> sO / sW[l & 1] (threads < kQM; coords from sC, so the
-  // caller orders this after a barrier that follows the sC stores)
-  auto decode = [&](int l) {
-    if (tid < kQM) {
-      int xs, ys;
-      float4 w4;
-      window_origin(sC[tid].x, sC[tid].y, 1.0f / static_cast<float>(1 << l), R, xs, ys, w4);  // 1/2^l exact (corr.py:68)
-      sO[l & 1][tid] = make_int2(xs, ys);
-      sW[l & 1][tid] = w4;
-    }
-  };
-  decode(0);
   // A's taps past KK (the last group's tail) are never written again: zero the whole A buffer once
   for (int e = tid; e < A_BYTES / 16; e += kNT) reinterpret_cast<u32x4*>(sA)[e] = u32x4{0u, 0u, 0u, 0u};
   __syncthreads();
-
-  // level geometry without dynamic indexing of the kernel arguments
-  auto level = [&](int l, int& Hl, int& Wl, int& WB, int& LF, const float*& base) {
-    Hl = a.Hl[0]; Wl = a.Wl[0]; WB = a.WB[0]; LF = a.LF[0]; base = a.lv[0];
-#pragma unroll
-    for (int j = 1; j < OFLOW_MAX_LEVELS; ++j)
-      if (j == l) { Hl = a.Hl[j]; Wl = a.Wl[j]; WB = a.WB[j]; LF = a.LF[j]; base = a.lv[j]; }
+  // chunk item s of this thread -> (query, window row, chunk): recomputed per use (a few full-rate ops; no live
+  // registers across the level)
+  static_assert(magic16_ok(PK * NCH, CITEMS) && magic16_ok(NCH, PK * NCH), "chunk item decode");
+  auto item_of = [&](int s, int& q, int& u, int& k) {
+    int t_ = tid;
+    asm volatile("" : "+v"(t_));
+    const unsigned item = static_cast<unsigned>(min(t_ + kNT * s, CITEMS - 1));
+    q = static_cast<int>(__umul24(item, magic16(PK * NCH)) >> 16);
+    const unsigned rm = item - static_cast<unsigned>(q) * (PK * NCH);
+    u = static_cast<int>(__umul24(rm, magic16(NCH)) >> 16);
+    k = static_cast<int>(rm - static_cast<unsigned>(u) * NCH);
   };
-  float rv[GI];
-  unsigned okm = 0u;  // bit s: gather item s is inside its level
-  static_assert(GI <= 32, "okm bits");
-  u32x4 rb[BI];
-  // gather level l's patches into rv (item = (query, patch row u, patch column c))
+
+  u32x4 rv[NI];
   auto gather = [&](int l) {
     int Hl, Wl, WB, LF;
     const float* base;
     level(l, Hl, Wl, WB, LF, base);
-    // the workgroup's queries of the level as one buffer; a tap outside the level loads the query block's first
-    // float and is zeroed through okm when staged (no exec branches: vmcnt is counted exactly; the buffer's
-    // out-of-range zero fill is not relied on)
     const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
         const_cast<float*>(base + (size_t)q0 * LF), (short)0, nq * LF * 4, 0x00020000);
-    int t = tid;
-    asm volatile("" : "+v"(t));  // opaque per call: the item decode below is recomputed, not hoisted into 25 live regs
-    okm = 0u;
+    constexpr int HB = (NI + 1) / 2;  // two batches of window reads: fewer live registers
 #pragma unroll
-    for (int s = 0; s < GI; ++s) {
-      const int item = min(t + kNT * s, kQM * PS - 1);
-      const int q = item / PS;
-      const int rm = item - q * PS;
-      const int u = rm / PK, c = rm - u * PK;
-      const int2 o = sO[l & 1][q];
-      const int y = o.y + u, x = o.x + c;
-      const bool ok = static_cast<unsigned>(y) < static_cast<unsigned>(Hl) && static_cast<unsigned>(x) < static_cast<unsigned>(Wl);
-      const int off = ok ? (q * LF + ((y >> 2) * WB + (x >> 3)) * 32 + ((y & 3) << 3) + (x & 7)) * 4 : 0;
-      okm |= (ok ? 1u : 0u) << s;
-      rv[s] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, off, 0, 0));
+    for (int s0 = 0; s0 < NI; s0 += HB) {
+      int4 o[NI];
+      int qs[NI], us[NI], ks[NI];
+#pragma unroll
+      for (int s = s0; s < (NI < s0 + HB ? NI : s0 + HB); ++s) {
+        item_of(s, qs[s], us[s], ks[s]);
+        o[s] = sO[l & (NS - 1)][qs[s]];
+      }
+#pragma unroll
+      for (int s = s0; s < (NI < s0 + HB ? NI : s0 + HB); ++s) {
+        const int q = qs[s], u = us[s], k = ks[s];
+        const int y = o[s].y + u, xc = (o[s].x - o[s].w) + 4 * k;
+        // the chunk holds a needed, in-level cell: row u valid, one of its 4 columns valid and inside the window
+        const unsigned need = ((static_cast<unsigned>(o[s].z) >> 16) >> u) & 1u &
+                              (((static_cast<unsigned>(o[s].z) & 0xffffu) >> (4 * k)) & 15u ? 1u : 0u) &
+                              (4 * k < o[s].w + PK ? 1u : 0u);
+        int off = (__umul24(q, LF) + (__umul24(static_cast<unsigned>(y) >> 2, WB) + (xc >> 3)) * 32 + ((y & 3) << 3) + (xc & 7)) * 4;
+        asm volatile("" : "+v"(off));  // computed unconditionally: a select, not an exec branch around it
+        off = need ? off : 0;
+        rv[s] = __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0);
+      }
     }
   };
-  // one k32 group of weights (256 channels x 128 B) per step: chunk c -> channel c / 8, 16-B slot c % 8
-  auto load_w = [&](int l, int g) {
-    const uint8_t* wg = a.w + (size_t)(l * G + g) * (kN * 128);
+  const __amdgpu_buffer_rsrc_t rsW =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(a.wf), (short)0, a.nlev * G * kN * 128, 0x00020000);
+  const int wbase = wn * 8192 + lane * 16;
+  u32x4 bq[2][8];  // B ring: global k32 group t in bq[t & 1]; [(nt * 2 + sub) * 2 + hi/lo]
+  auto load_b = [&](int t, u32x4 (&dst)[8]) {
+    const int so = t * (kN * 128);
 #pragma unroll
-    for (int s = 0; s < BI; ++s) rb[s] = *reinterpret_cast<const u32x4*>(wg + (size_t)(tid + kNT * s) * 16);
+    for (int e = 0; e < 8; ++e) dst[e] = __builtin_amdgcn_raw_buffer_load_b128(rsW, wbase, so + e * 1024, 0);
   };
-  auto write_w = [&]() {
-#pragma unroll
-    for (int s = 0; s < BI; ++s) {
-      const int c = tid + kNT * s, n = c >> 3, sl = c & 7;
-      *reinterpret_cast<u32x4*>(sB + n * 128 + ((sl ^ swz(n)) << 4)) = rb[s];
-    }
-  };
-
   f32x16 acc[2][2];
 #pragma unroll
   for (int i = 0; i < 2; ++i)
@@ -169,38 +214,56 @@ __global__ __launch_bounds__(kNT, 2) void corr_convc1_kernel(C1Args a) {
 #pragma unroll
       for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
 
-  load_w(0, 0);
+  const int nlg = a.nlev * G;
+  load_b(0, bq[0]);
+  if (nlg > 1) load_b(1, bq[1]);
   gather(0);
-  for (int l = 0; l < a.nlev; ++l) {
-    // ---- 1. patches -> LDS (over the weight buffer: the previous level's MFMAs are done) ----
+  stamp();
+  // one level; P = (l * G) & 1: the ring slot of the level's first group
+  auto body = [&](int l, auto Pc) {
+    constexpr int P = decltype(Pc)::value;
+    // ---- 1. chunks -> LDS patches (cells outside the level zeroed) ----
 #pragma unroll
-    for (int s = 0; s < GI; ++s) {
-      const int item = tid + kNT * s;
-      if (item < kQM * PS) {
-        const int q = item / PS;
-        sP[q * QS + (item - q * PS)] = ((okm >> s) & 1u) ? rv[s] : 0.0f;
+    for (int s = 0; s < NI; ++s) {
+      if (CITEMS % kNT == 0 || tid + kNT * s < CITEMS) {
+        int q, u, k;
+        item_of(s, q, u, k);
+        const int4 o = sO[l & (NS - 1)][q];
+        const unsigned m = (((static_cast<unsigned>(o.z) >> 16) >> u) & 1u) ? ((static_cast<unsigned>(o.z) >> (4 * k)) & 15u) : 0u;
+        const float* fv = reinterpret_cast<const float*>(&rv[s]);
+        float* dst = sP + q * QS + u * RW + 3 + 4 * k - o.w;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) dst[e] = ((m >> e) & 1u) ? fv[e] : 0.0f;
       }
     }
-    __syncthreads();
-    // ---- 2. bilinear taps -> split-fp16 A operand: thread = (pixel q, slots S = set, set + 4, ...) ----
+    __syncthreads();  // patches complete; every wave is past level l-1's MFMAs (A free)
+    stamp();
+    // ---- 2. next level's gathers (rv is free), the level after next's windows ----
+    if (l + 1 < a.nlev) gather(l + 1);
+    if (tid < kQM && l + 2 < a.nlev) decode(l + 2, sC[tid].x, sC[tid].y);
+    // ---- 3. bilinear taps -> split-fp16 A operand; the slot set is the wave index (a scalar branch per slot) ----
     {
-      const int q = tid & (kQM - 1), set = tid / kQM;  // set (= wave) is uniform per wave
-      const float4 w4 = sW[l & 1][q];
-      const float* p = sP + q * QS;
+      const int q = tid & (kQM - 1), set = __builtin_amdgcn_readfirstlane(tid / kQM);
+      const float4 w4 = sW[l & (NS - 1)][q];
+      const float* p = sP + q * QS + 3;
 #pragma unroll
       for (int S = 0; S < NSLOT; ++S) {
         if ((S & 3) != set) continue;
-        half8 hi, lo;
+        float v[8];  // all 8 taps first (the shared cells are read once), then the splits
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
           const int k = 8 * S + e;  // reference channel order within the level: k = i*K + j, i moves x, j moves y
-          float v = 0.f;
+          v[e] = 0.f;
           if (k < KK) {
             const int i = k / K, j = k - (k / K) * K;
-            v = bilinear4(p[j * PK + i], p[j * PK + i + 1], p[(j + 1) * PK + i], p[(j + 1) * PK + i + 1], w4);
+            v[e] = bilinear4(p[j * RW + i], p[j * RW + i + 1], p[(j + 1) * RW + i], p[(j + 1) * RW + i + 1], w4);
           }
+        }
+        half8 hi, lo;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
           _Float16 h_, l_;
-          split_f16(v, h_, l_);
+          split_f16(v[e], h_, l_);
           hi[e] = h_;
           lo[e] = l_;
         }
@@ -209,58 +272,48 @@ __global__ __launch_bounds__(kNT, 2) void corr_convc1_kernel(C1Args a) {
         *reinterpret_cast<half8*>(row + (((4 + (S & 3)) ^ swz(q)) << 4)) = lo;
       }
     }
-    if (l + 1 < a.nlev) decode(l + 1);
-    __syncthreads();  // patches dead (the weight buffer is free), A complete, the next level's windows decoded
-    // ---- 3. the level's k32 groups: weights (held in rb since the previous group) -> LDS, the next group's (or the
-    // next level's first) weights loaded, then the group's MFMAs. The next level's gathers are issued after the
-    // level's last weight load (vmcnt retires in order: a weight wait never waits for them) and fly during the last
-    // group's MFMAs; the other workgroup on the CU covers what they do not hide. ----
-    half8 ah[2][2], al[2][2], bh[2][2], bl[2][2];  // [sub-step][tile]
-    auto read_ops = [&](int g, int sub) {
-      const int chi = 2 * sub + hh, clo = 4 + 2 * sub + hh;
-#pragma unroll
-      for (int mt = 0; mt < 2; ++mt) {
-        const int pr = mt * 32 + r;
-        const uint8_t* row = sA + g * (kQM * 128) + pr * 128;
-        ah[sub][mt] = *reinterpret_cast<const half8*>(row + ((chi ^ swz(pr)) << 4));
-        al[sub][mt] = *reinterpret_cast<const half8*>(row + ((clo ^ swz(pr)) << 4));
-      }
-#pragma unroll
-      for (int nt = 0; nt < 2; ++nt) {
-        const int n = wn * 64 + nt * 32 + r;
-        const uint8_t* row = sB + n * 128;
-        bh[sub][nt] = *reinterpret_cast<const half8*>(row + ((chi ^ swz(n)) << 4));
-        bl[sub][nt] = *reinterpret_cast<const half8*>(row + ((clo ^ swz(n)) << 4));
-      }
-    };
+    __syncthreads();  // A complete; the patches consumed
+    stamp();
+    // ---- 4. the level's MFMAs ----
 #pragma unroll
     for (int g = 0; g < G; ++g) {
-      write_w();
-      if (g + 1 < G) {
-        load_w(l, g + 1);
-      } else if (l + 1 < a.nlev) {
-        load_w(l + 1, 0);
-        gather(l + 1);
-      }
-      __syncthreads();  // group g's weights visible
-      read_ops(g, 0);
-      read_ops(g, 1);
+      constexpr int dummy = 0;
+      (void)dummy;
+      u32x4 (&bc)[8] = bq[(P + g) & 1];
 #pragma unroll
-      for (int sub = 0; sub < 2; ++sub)
+      for (int sub = 0; sub < 2; ++sub) {
+        half8 ah[2], al[2];
+        const int chi = 2 * sub + hh, clo = 4 + 2 * sub + hh;
+#pragma unroll
+        for (int mt = 0; mt < 2; ++mt) {
+          const int pr = mt * 32 + r;
+          const uint8_t* row = sA + g * (kQM * 128) + pr * 128;
+          ah[mt] = *reinterpret_cast<const half8*>(row + ((chi ^ swz(pr)) << 4));
+          al[mt] = *reinterpret_cast<const half8*>(row + ((clo ^ swz(pr)) << 4));
+        }
 #pragma unroll
         for (int mt = 0; mt < 2; ++mt)
 #pragma unroll
           for (int nt = 0; nt < 2; ++nt) {
-            acc[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[sub][mt], bl[sub][nt], acc[mt][nt], 0, 0, 0);
-            acc[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[sub][mt], bh[sub][nt], acc[mt][nt], 0, 0, 0);
-            acc[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[sub][mt], bh[sub][nt], acc[mt][nt], 0, 0, 0);
+            const half8 bh = __builtin_bit_cast(half8, bc[(nt * 2 + sub) * 2 + 0]);
+            const half8 bl = __builtin_bit_cast(half8, bc[(nt * 2 + sub) * 2 + 1]);
+            acc[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[mt], bl, acc[mt][nt], 0, 0, 0);
+            acc[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[mt], bh, acc[mt][nt], 0, 0, 0);
+            acc[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[mt], bh, acc[mt][nt], 0, 0, 0);
           }
-      __syncthreads();  // group g's operand reads done: the weight buffer (and at the level's end the patch / A
-                        // buffers) may be overwritten
+      }
+      const int t2 = l * G + g + 2;  // the ring slot is free: the group two ahead
+      if (t2 < nlg) load_b(t2, bc);
     }
+    stamp();
+  };
+  for (int l = 0; l < a.nlev; l += 2) {
+    body(l, std::integral_constant<int, 0>{});  // (l * G) & 1 = 0 for even l
+    if (l + 1 < a.nlev) body(l + 1, std::integral_constant<int, G & 1>{});
   }
 
   // ---- epilogue: accumulators -> LDS tile [pixel][channel] -> scale, bias, ReLU -> S32 ----
+  __syncthreads();  // every wave is past its last A read (the tile overlays A and the patches)
   float* sT = reinterpret_cast<float*>(smem);
 #pragma unroll
   for (int mt = 0; mt < 2; ++mt)
@@ -271,9 +324,16 @@ __global__ __launch_bounds__(kNT, 2) void corr_convc1_kernel(C1Args a) {
 #pragma unroll
       for (int e = 0; e < 16; ++e) sT[(pbase + (e & 3) + 8 * (e >> 2) + 4 * hh) * TS + n] = acc[mt][nt][e];
     }
+  // each thread's 8 channels are the same for every item (kNT is a multiple of kN / 8): their (scale, bias) once
+  static_assert(kNT % (kN / 8) == 0, "fixed channel octet per thread");
+  const int n = (tid % (kN / 8)) * 8;
+  float2 sbv[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) sbv[j] = sSB[n + j];
   __syncthreads();
-  for (int item = tid; item < kQM * (kN / 8); item += kNT) {
-    const int pl = item / (kN / 8), n = (item - pl * (kN / 8)) * 8;
+#pragma unroll
+  for (int it = 0; it < kQM * (kN / 8) / kNT; ++it) {
+    const int pl = (tid + it * kNT) / (kN / 8);
     if (pl >= nq) continue;
     const float4 t0 = *reinterpret_cast<const float4*>(&sT[pl * TS + n]);
     const float4 t1 = *reinterpret_cast<const float4*>(&sT[pl * TS + n + 4]);
@@ -281,7 +341,7 @@ __global__ __launch_bounds__(kNT, 2) void corr_convc1_kernel(C1Args a) {
     half8 hi, lo;
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-      const float2 sb = sSB[n + j];
+      const float2 sb = sbv[j];
       float x = v[j] * sb.x + sb.y;
       x = x < 0.f ? 0.f : x;  // relu (update.py:120); NaN propagates like ATen
       _Float16 h_, l_;
@@ -293,7 +353,11 @@ __global__ __launch_bounds__(kNT, 2) void corr_convc1_kernel(C1Args a) {
     *reinterpret_cast<half8*>(line) = hi;
     *reinterpret_cast<half8*>(line + 64) = lo;
   }
+  if (a.stamps != nullptr) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  stamp();
 }
+
+unsigned long long* g_convc1_stamps = nullptr;  // diagnostics (experiment hook): per-workgroup clock stamps
 
 }  // namespace
 }  // namespace oflow
@@ -319,21 +383,28 @@ extern "C" int oflow_corr_lookup_convc1_s32(const float* const* d_levels, const 
     a.Wl[l] = level_w[l];
     a.WB[l] = (level_w[l] + 7) / 8;
     a.LF[l] = ((level_h[l] + 3) / 4) * a.WB[l] * 32;
+    if ((long long)kQM * a.LF[l] * 4 >= (1ll << 31)) return OFLOW_E_SHAPE;  // a workgroup's window reads: 32-bit offsets
   }
   a.nlev = num_levels;
   a.coords = d_coords;
   a.N = H * W;
   a.total = B * H * W;
-  a.w = static_cast<const uint8_t*>(d_wpack);
+  a.wf = static_cast<const uint8_t*>(d_wpack);
   a.wsc = d_wscale;
   a.bias = d_bias;
   a.y = static_cast<uint8_t*>(d_y);
   a.yps = y_pixel_stride;
   const dim3 grid((a.total + kQM - 1) / kQM);
   hipStream_t s = static_cast<hipStream_t>(stream);
+  a.stamps = g_convc1_stamps;
   if (radius == 4)
     hipLaunchKernelGGL((corr_convc1_kernel<4>), grid, dim3(kNT), 0, s, a);
   else
     hipLaunchKernelGGL((corr_convc1_kernel<3>), grid, dim3(kNT), 0, s, a);
   return launch_status();
+}
+
+// experiment hook (not part of include/oflow.h): a device buffer of 16 clock stamps per workgroup, or null
+extern "C" void oflow_exp_set_convc1_stamps(void* stamps) {
+  oflow::g_convc1_stamps = static_cast<unsigned long long*>(stamps);
 }

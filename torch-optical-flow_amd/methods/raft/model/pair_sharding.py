@@ -54,6 +54,11 @@ def scatter_pairs(
     ``shape`` = the global (B, C, H, W) when every rank knows it (fixed per run: no metadata collective, no host
     sync); otherwise it is broadcast from ``src``."""
     world, rank = _world(group)
+    if shape is not None and rank == src:
+        # host-only check (no collective, no sync): a wrong ``shape`` would mis-size the scatter silently
+        for img in (image0, image1):
+            if tuple(img.shape) != tuple(shape):
+                raise ValueError(f"scatter_pairs: shape {tuple(shape)} does not match the source batch {tuple(img.shape)}")
     shape = list(shape) if shape is not None else _meta(image0, src, group, device)
     b, rest = shape[0], shape[1:]
     chunk = -(-b // world)

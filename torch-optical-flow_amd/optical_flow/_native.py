@@ -698,7 +698,7 @@ class ConvWeights:
     """A conv layer's weights packed for oflow_conv_s32: [in_groups][taps][n_pad][hi | lo] fp16 (per-output-channel
     power-of-two scaled so that max |w| = 2^14 keeps the lo halves normal), the inverse scales and the bias."""
 
-    __slots__ = ("pack", "wscale", "bias", "n", "n_pad", "kh", "kw", "kg")
+    __slots__ = ("pack", "wscale", "bias", "n", "n_pad", "kh", "kw", "kg", "layout")
 
     def __init__(self, weight: torch.Tensor, bias, n_pad: int, patches: bool = False):
         w = weight.detach().float()
@@ -725,6 +725,7 @@ class ConvWeights:
         self.wscale = inv
         self.bias = None if bias is None else bias.detach().float().contiguous()
         self.n, self.n_pad, self.kh, self.kw, self.kg = n, n_pad, kh, kw, kg
+        self.layout = "conv"  # "convc1_frag": convc1_level_weights (the fused lookup + convc1's fragment-major order)
 
 
 def convc1_level_weights(conv: torch.nn.Conv2d, num_levels: int, radius: int) -> "ConvWeights":
@@ -738,7 +739,13 @@ def convc1_level_weights(conv: torch.nn.Conv2d, num_levels: int, radius: int) ->
     wp = w.new_zeros((w.shape[0], num_levels * g * 32, 1, 1))
     for l in range(num_levels):
         wp[:, l * g * 32 : l * g * 32 + kk] = w[:, l * kk : (l + 1) * kk]
-    return ConvWeights(wp, conv.bias, w.shape[0])
+    cw = ConvWeights(wp, conv.bias, w.shape[0])
+    # fragment-major (include/oflow.h): [group][n 256][hi, lo][k 32] -> [group][wave][ntile][sub][hi, lo][hh][r][8]
+    lg = cw.pack.shape[0]
+    frag = cw.pack.reshape(lg, 4, 2, 32, 2, 2, 2, 8)  # group, wave, ntile, r, hi/lo, sub, hh, 8
+    cw.pack = frag.permute(0, 1, 2, 5, 4, 6, 3, 7).contiguous()
+    cw.layout = "convc1_frag"
+    return cw
 
 
 def corr_lookup_convc1(pyr: "TiledPyramid", coords: torch.Tensor, radius: int, cw: "ConvWeights", y: "S32Slice") -> None:
@@ -751,7 +758,8 @@ def corr_lookup_convc1(pyr: "TiledPyramid", coords: torch.Tensor, radius: int, c
     if two != 2 or b * h * w != pyr.queries:
         raise RuntimeError(f"{what}: coords (B, 2, H, W) must cover the pyramid's {pyr.queries} queries")
     kk = (2 * radius + 1) ** 2
-    if cw.n != 256 or cw.n_pad != 256 or cw.kh * cw.kw != 1 or cw.kg != len(pyr.levels) * ((kk + 31) // 32):
+    if (cw.layout != "convc1_frag" or cw.n != 256 or cw.n_pad != 256 or cw.kh * cw.kw != 1
+            or cw.kg != len(pyr.levels) * ((kk + 31) // 32)):
         raise RuntimeError(f"{what}: weights must be convc1_level_weights of this pyramid / radius")
     if y.ng != 8 or y.bhw != (b, h, w) or y.device != co.device:
         raise RuntimeError(f"{what}: destination must be an 8-group S32 slice of shape ({b}, {h}, {w})")

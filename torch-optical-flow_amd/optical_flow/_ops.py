@@ -77,6 +77,15 @@ def _pyramid_backward(ctx, grads):
 
 def _lookup_setup(ctx, inputs, output):
     levels, coords, radius = inputs
+    # the native transpose rebuilds every level's size from level 0 by floor 2x2 pooling (corr.py:53): levels of any
+    # other size are refused here, in the forward, instead of failing with a gradient-shape error in the backward
+    h, w = (int(v) for v in levels[0].shape[-2:])
+    for lv in levels:
+        if tuple(int(v) for v in lv.shape[-2:]) != (h, w):
+            raise RuntimeError(
+                f"corr_lookup backward: level sizes must be the floor 2x2 pools of level 0 (expected {(h, w)}, got "
+                f"{tuple(lv.shape[-2:])})")
+        h, w = h // 2, w // 2
     ctx.save_for_backward(coords)
     ctx.radius = radius
     ctx.level0 = tuple(levels[0].shape[-2:])
