@@ -55,6 +55,7 @@ extern "C" {
 #define OFLOW_IN_S32 0
 #define OFLOW_IN_F32_NORM 1
 #define OFLOW_IN_F32 2
+#define OFLOW_IN_IMG7S2 3
 
 int oflow_abi_version(void);
 const char* oflow_status_string(int status);
@@ -237,6 +238,11 @@ int oflow_corr_lookup_convc1_s32(const float* const* d_levels, const int* level_
  *   in_groups <= 4); OFLOW_IN_F32: an fp32 NHWC input of cin = x_pixel_stride/4 channels per pixel
  *   ((in_groups-1)*32 < cin <= in_groups*32, x_pixel_stride % 16 == 0; channels past cin stage as zeros) split into
  *   hi + lo while staged (1x1, epilogue 0, block_n 128: convc1 reading oflow_corr_lookup_tiled_nhwc_f32's rows).
+ *   OFLOW_IN_IMG7S2: the encoders' stem (extractor.py:186, a 7x7 / stride 2 / pad 3 conv of a 3-channel image) straight
+ *   from the fp32 NCHW image d_x (B, 3, 2H, 2W) for an output of H x W (x_pixel_stride ignored): each 4 x 32 output tile
+ *   stages its 13 x 69 x 3 input window in LDS and builds the patch-matrix operand (channel t*3 + c, t = ky*7 + kx,
+ *   in_groups 5 = 160 channels, weights packed with patches=True as for oflow_stem_patches_s32's matrix) from it, so
+ *   no patch matrix is written (1x1 geometry, epilogue 0, block_n 64).
  * oflow_stem_patches_s32: 7x7/2 pad-3 patch matrix of a (B, C, H, W) fp32 image: S32 (B, ceil(H/2), ceil(W/2),
  *   out_groups) with channel t*C + c (t = ky*7 + kx), zeros past 49*C.
  * oflow_norm_stats_finalize: merge the partials (fp64 sums) -> alpha = 1/sqrt(var + eps), beta = -mean * alpha, [B][C].
@@ -302,6 +308,28 @@ int oflow_corr_lookup_backward_f32(const float* d_grad_out, const float* d_coord
                                    void* stream);
 int oflow_corr_pyramid_grad_combine_f32(float* const* d_grad_levels, const int* level_h, const int* level_w,
                                         int num_levels, long long Q, void* stream);
+/* oflow_corr_fmap_grad_f32: the feature-map gradients of corr.py:85 (corr = f1^T f2 / sqrt(C)) from the level-0-folded
+ *   gradient g0 (B, N, N) (query-major): d_grad_f1 (B, C, N) = scale * f2 . g0^T, d_grad_f2 (B, C, N) = scale * f1 . g0
+ *   (scale = 1/sqrt(C)), fmaps (B, C, N) fp32; fp32 MFMA GEMMs, deterministic. Either output may be NULL. */
+int oflow_corr_fmap_grad_f32(const float* d_fmap1, const float* d_fmap2, const float* d_g0, int B, int C, int N,
+                             float scale, float* d_grad_f1, float* d_grad_f2, void* stream);
+
+/*
+ * Backward of the warp / grid_sample (optical_flow/operator/operator.py:8-56, utils.py:64-80 under autograd; SURVEY
+ * §8(f) row 3; csrc/warp_backward.hip): ATen grid_sampler_2d_backward's formulas for every mode / padding /
+ * align_corners. d_grad_frame / d_grad_input must be zero-filled by the caller (taps are added with fp32 atomics);
+ * either output may be NULL.
+ * oflow_grid_warp_backward_f32: d_grad_out (B, C, H, W), frame (B, C, H, W), normalized flow (B, 2, H, W) ->
+ *   d_grad_frame (B, C, H, W) += ..., d_grad_flow (B, 2, H, W) = dL/d(grid) (grid = linspace base + flow).
+ * oflow_grid_sample_backward_f32: d_grad_out (B, C, Ho, Wo), input (B, C, H, W), grid (B, Ho, Wo, 2) ->
+ *   d_grad_input += ..., d_grad_grid (B, Ho, Wo, 2).
+ */
+int oflow_grid_warp_backward_f32(const float* d_grad_out, const float* d_frame, const float* d_flow, int B, int C, int H,
+                                 int W, int mode, int padding_mode, int align_corners, float* d_grad_frame,
+                                 float* d_grad_flow, void* stream);
+int oflow_grid_sample_backward_f32(const float* d_grad_out, const float* d_input, const float* d_grid, int B, int C,
+                                   int H, int W, int Ho, int Wo, int mode, int padding_mode, int align_corners,
+                                   float* d_grad_input, float* d_grad_grid, void* stream);
 
 /*
  * Inference I/O (csrc/flow_io.hip).

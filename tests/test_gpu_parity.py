@@ -363,17 +363,61 @@ def test_inference_layouts_refuse_autograd_inputs():
         assert optical_flow.warp(frame, flow).shape == frame.shape
 
 
+@pytest.mark.parametrize("ac", [False, True])
+@pytest.mark.parametrize("mode", ["bilinear", "nearest", "bicubic"])
 @pytest.mark.parametrize("pad", ["zeros", "border", "reflection"])
-def test_warp_autograd_matches_oracle(pad):
-    """optical_flow.warp under autograd: HIP forward, grid_sampler backward -- frame and flow gradients equal the
-    reference operator's (operator.py:8-56) on the CPU."""
+def test_warp_autograd_matches_oracle(pad, mode, ac):
+    """optical_flow.warp under autograd: HIP forward, native backward (warp_backward.hip) -- frame and flow gradients
+    equal the reference operator's (operator.py:8-56) differentiated on the CPU, every mode / padding / align_corners,
+    with flows that push taps past every border."""
     img0, _ = synthetic.synthetic_pair(2, 40, 64, seed=9)
-    flow = oop.normalize(torch.from_numpy(synthetic.hash_normal(13, (2, 2, 40, 64), 3.0)))
+    flow = oop.normalize(torch.from_numpy(synthetic.hash_normal(13, (2, 2, 40, 64), 6.0)))
     r = torch.from_numpy(synthetic.hash_normal(14, (2, 3, 40, 64), 1.0))
     a_f, a_w = img0.clone().requires_grad_(), flow.clone().requires_grad_()
-    (oop.warp(a_f, a_w, "bilinear", pad, False) * r).sum().backward()
+    (oop.warp(a_f, a_w, mode, pad, ac) * r).sum().backward()
     d_f, d_w = img0.to(DEV).requires_grad_(), flow.to(DEV).requires_grad_()
-    (optical_flow.warp(d_f, d_w, "bilinear", pad) * r.to(DEV)).sum().backward()
-    assert float((d_f.grad.cpu() - a_f.grad).abs().max()) <= 1e-4
+    (optical_flow.warp(d_f, d_w, mode, pad, ac) * r.to(DEV)).sum().backward()
+    gf = float(a_f.grad.abs().max())
+    assert float((d_f.grad.cpu() - a_f.grad).abs().max()) <= 1e-5 * gf + 1e-4
     gw = float(a_w.grad.abs().max())
     assert float((d_w.grad.cpu() - a_w.grad).abs().max()) <= 1e-3 * gw + 1e-3
+
+
+@pytest.mark.parametrize("mode", ["bilinear", "nearest", "bicubic"])
+@pytest.mark.parametrize("pad", ["zeros", "border", "reflection"])
+def test_grid_sample_autograd_matches_oracle(pad, mode):
+    """torch.ops.oflow.grid_sample (bilinear_sampler's explicit grid, utils.py:64-80) under autograd with the native
+    backward vs F.grid_sample differentiated on the CPU: input and grid gradients, an output size other than the
+    input's, grid values past [-1, 1]."""
+    g = torch.Generator().manual_seed(3)
+    x = torch.randn(2, 5, 17, 23, generator=g)
+    grid = torch.rand(2, 11, 13, 2, generator=g) * 2.6 - 1.3
+    r = torch.randn(2, 5, 11, 13, generator=g)
+    a_x, a_g = x.clone().requires_grad_(), grid.clone().requires_grad_()
+    (torch.nn.functional.grid_sample(a_x, a_g, mode=mode, padding_mode=pad, align_corners=True) * r).sum().backward()
+    d_x, d_g = x.to(DEV).requires_grad_(), grid.to(DEV).requires_grad_()
+    out = torch.ops.oflow.grid_sample(d_x, d_g, _native.INTERP[mode], _native.PADDING[pad], True)
+    (out * r.to(DEV)).sum().backward()
+    assert float((d_x.grad.cpu() - a_x.grad).abs().max()) <= 1e-5 * float(a_x.grad.abs().max()) + 1e-5
+    assert float((d_g.grad.cpu() - a_g.grad).abs().max()) <= 1e-4 * float(a_g.grad.abs().max()) + 1e-4
+
+
+@pytest.mark.parametrize("b,c,n", [(2, 256, 1000), (1, 32, 792), (3, 70, 130)])
+def test_fmap_gradient_gemms_match_fp64(b, c, n):
+    """The fmap gradients of the correlation (corr.py:85 transposed) on fp32 MFMA (oflow_corr_fmap_grad_f32 through
+    corr_pyramid_backward, one level) vs float64: grad_f1 = f2 . G^T / sqrt(C), grad_f2 = f1 . G / sqrt(C); ragged
+    64-tiles in C and N."""
+    g = torch.Generator().manual_seed(c + n)
+    h, w = 1, n
+    f1 = torch.randn(b, c, h, w, generator=g)
+    f2 = torch.randn(b, c, h, w, generator=g)
+    g0 = torch.randn(b * n, 1, h, w, generator=g)
+    g1, g2 = torch.ops.oflow.corr_pyramid_backward([g0.to(DEV)], f1.to(DEV), f2.to(DEV))
+    G = g0.double().view(b, n, n)
+    s = 1.0 / math.sqrt(c)
+    r1 = torch.bmm(f2.double().view(b, c, n), G.transpose(1, 2)) * s
+    r2 = torch.bmm(f1.double().view(b, c, n), G) * s
+    bound1 = torch.bmm(f2.double().abs().view(b, c, n), G.abs().transpose(1, 2)) * s
+    bound2 = torch.bmm(f1.double().abs().view(b, c, n), G.abs()) * s
+    assert bool(((g1.cpu().double().view(b, c, n) - r1).abs() <= 2e-5 * bound1 + 1e-6).all())
+    assert bool(((g2.cpu().double().view(b, c, n) - r2).abs() <= 2e-5 * bound2 + 1e-6).all())

@@ -213,6 +213,26 @@ def test_split_encoder_matches_module(norm, b, h, w):
     assert err <= 1e-4 * max(1.0, scale), err
 
 
+@pytest.mark.parametrize("norm", ["instance", "batch"])
+@pytest.mark.parametrize("b,h,w", [(2, 128, 160), (1, 440, 1024), (3, 72, 88)])
+def test_split_encoder_stem_from_image_bit_identical(norm, b, h, w):
+    """The stem conv building its 7x7/2 patch operand from the staged image window (OFLOW_IN_IMG7S2) gives the patch
+    matrix path's encoder output bit for bit (same operand values, same k order): ragged 4x32 tiles (72x88 input ->
+    36x44 stem output), image borders (zero padding), both norms."""
+    from model.extractor import SplitEncoder
+
+    model = _model(RAFT)
+    enc = model.fnet if norm == "instance" else model.cnet
+    img0, _ = synthetic.synthetic_pair(b, h, w, seed=4)
+    x = (2 * (img0.to(DEV) / 255.0) - 1.0).contiguous()
+    with torch.inference_mode():
+        a = SplitEncoder(enc)(x)
+        c = SplitEncoder(enc)(x, stem_from_image=True)
+        sa = SplitEncoder(enc)(x, split_out=True)
+        sc = SplitEncoder(enc)(x, split_out=True, stem_from_image=True)
+    assert torch.equal(a, c) and torch.equal(sa, sc)
+
+
 @pytest.mark.parametrize("shape", [(2, 55, 128), (1, 1, 1), (3, 7, 33), (1, 47, 156)])
 def test_convex_upsample_matches_oracle(shape):
     """RAFT.upsample_flow on the GPU (one fused kernel, csrc/upsample.hip) vs the reference formula (raft.py:73-85) on

@@ -81,7 +81,9 @@ struct ConvArgs {
   int wbytes;              // bytes of the packed weights (kg * taps * npad * 128)
 };
 // input formats of oflow_conv_s32_ex2
-constexpr int kInS32 = OFLOW_IN_S32, kInF32Norm = OFLOW_IN_F32_NORM, kInF32 = OFLOW_IN_F32;
+constexpr int kInS32 = OFLOW_IN_S32, kInF32Norm = OFLOW_IN_F32_NORM, kInF32 = OFLOW_IN_F32, kInImg = OFLOW_IN_IMG7S2;
+// kInImg: the stem's 7x7/2 pad-3 window of a 3-channel image, staged per tile (TY = 4 rows x 32 columns)
+constexpr int kImgC = 3, kImgK = 7, kImgRows = (kTY - 1) * 2 + kImgK, kImgCols = (kTX - 1) * 2 + kImgK;
 
 __device__ __forceinline__ float act_fn(float v, int act) {
   if (act == 1) return v < 0.f ? 0.f : v;  // relu; NaN propagates like ATen
@@ -158,12 +160,16 @@ __global__ __launch_bounds__(64 * WM * WN, WM * WN == 8 ? 1 : 2) void conv_s32_k
   constexpr int TS = BN + 4;              // epilogue tile row stride (floats)
   constexpr int EPI_BYTES = BM * TS * 4;
   constexpr int LDS_BYTES = MAIN_BYTES > EPI_BYTES ? MAIN_BYTES : EPI_BYTES;
-  constexpr int AFF_BYTES = AIN == kInF32Norm ? kAinGroups * 32 * 8 : 0;  // float2 (scale, shift) per input channel
+  constexpr int AFF_BYTES = AIN == kInF32Norm ? kAinGroups * 32 * 8       // float2 (scale, shift) per input channel
+                            : AIN == kInImg ? kImgC * kImgRows * kImgCols * 4  // the stem's input window
+                            : 0;
+  static_assert(AIN != kInImg || (T == 1 && TY == kTY), "image input: 1x1 geometry over the patch channels, 4-row tiles");
   __shared__ __attribute__((aligned(16))) uint8_t smem[LDS_BYTES + AFF_BYTES];
   // the block's per-channel (inverse weight scale, bias), staged once for the epilogue (whose loops would otherwise
   // wait on a global-load round trip per iteration)
   __shared__ float2 sSB[BN];
   float2* sAff = reinterpret_cast<float2*>(smem + LDS_BYTES);
+  float* sImg = reinterpret_cast<float*>(smem + LDS_BYTES);  // kInImg: [c][row][col]
   uint8_t* sA = smem;
   uint8_t* sB = smem + (ADB ? 2 : 1) * A_BYTES;
 
@@ -217,7 +223,7 @@ __global__ __launch_bounds__(64 * WM * WN, WM * WN == 8 ? 1 : 2) void conv_s32_k
 #pragma unroll
   for (int s_ = 0; s_ < BPER; ++s_) boff[s_] = (n0 + (tid + s_ * NTH) / 8) * 128 + ((tid + s_ * NTH) & 7) * 16;
 #define OFLOW_LOAD_A(RA, G)                                                                                          \
-  _Pragma("unroll") for (int s_ = 0; s_ < APER; ++s_) {                                                              \
+  if constexpr (AIN != kInImg) _Pragma("unroll") for (int s_ = 0; s_ < APER; ++s_) {                                 \
     int col_;                                                                                                        \
     const int off_ = a_off(s_, col_);                                                                                \
     if constexpr (AIN == kInF32) /* rows of cin floats: channels past cin re-read the row's last 16 B (zeroed) */   \
@@ -234,7 +240,21 @@ __global__ __launch_bounds__(64 * WM * WN, WM * WN == 8 ? 1 : 2) void conv_s32_k
         /* 4 fp32 channels (G*32 + 4c ..) [-> relu(x * scale + shift)] -> 4 hi + 4 lo halves (8 B each) */           \
         typedef _Float16 half4_ __attribute__((ext_vector_type(4)));                                                 \
         half4_ h4 = {0, 0, 0, 0}, l4 = {0, 0, 0, 0};                                                                 \
-        if (((aok >> s_) & 1u) && (AIN != kInF32 || (G) * 32 + 4 * c < a.cin)) {                                    \
+        if constexpr (AIN == kInImg) {                                                                               \
+          /* patch channel k = t*3 + ch, t = ky*7 + kx, of pixel p: the staged window at (2*py + ky, 2*px + kx) */   \
+          const int py_ = p / kTX, px_ = p - py_ * kTX;                                                              \
+          _Pragma("unroll") for (int e_ = 0; e_ < 4; ++e_) {                                                         \
+            const int k_ = (G) * 32 + 4 * c + e_;                                                                    \
+            const int t_ = k_ / kImgC, ch_ = k_ - t_ * kImgC;                                                        \
+            const int ky_ = t_ / kImgK, kx_ = t_ - ky_ * kImgK;                                                      \
+            const float v_ = t_ < kImgK * kImgK                                                                      \
+                ? sImg[(ch_ * kImgRows + 2 * py_ + ky_) * kImgCols + 2 * px_ + kx_] : 0.f;                           \
+            _Float16 hv, lv;                                                                                         \
+            split_f16(v_, hv, lv);                                                                                   \
+            h4[e_] = hv;                                                                                             \
+            l4[e_] = lv;                                                                                             \
+          }                                                                                                          \
+        } else if (((aok >> s_) & 1u) && (AIN != kInF32 || (G) * 32 + 4 * c < a.cin)) {                             \
           const float* fv = reinterpret_cast<const float*>(&RA[s_]);                                                 \
           _Pragma("unroll") for (int e_ = 0; e_ < 4; ++e_) {                                                         \
             float v_ = fv[e_];                                                                                       \
@@ -318,6 +338,21 @@ __global__ __launch_bounds__(64 * WM * WN, WM * WN == 8 ? 1 : 2) void conv_s32_k
   if constexpr (AIN == kInF32Norm) {
     for (int e = tid; e < a.kg * 32; e += NTH)
       sAff[e] = make_float2(a.ia[(long long)b * a.kg * 32 + e], a.ib[(long long)b * a.kg * 32 + e]);
+    __syncthreads();
+  }
+  if constexpr (AIN == kInImg) {
+    // the tile's input window (rows 2*ty0 - 3 .., columns 2*tx0 - 3 ..), zero padded (extractor.py:186 padding=3)
+    const float* img = reinterpret_cast<const float*>(a.x) + (long long)b * kImgC * (2 * a.H) * (2 * a.W);
+    const int iy0 = 2 * ty0 - kImgK / 2, ix0 = 2 * tx0 - kImgK / 2;
+    for (int e = tid; e < kImgC * kImgRows * kImgCols; e += NTH) {
+      const int ch = e / (kImgRows * kImgCols), rem = e - ch * (kImgRows * kImgCols);
+      const int ry = rem / kImgCols, rx = rem - ry * kImgCols;
+      const int iy = iy0 + ry, ix = ix0 + rx;
+      float v = 0.f;
+      if (static_cast<unsigned>(iy) < static_cast<unsigned>(2 * a.H) && static_cast<unsigned>(ix) < static_cast<unsigned>(2 * a.W))
+        v = img[((long long)ch * (2 * a.H) + iy) * (2 * a.W) + ix];
+      sImg[e] = v;
+    }
     __syncthreads();
   }
   // prologue: step 0 in LDS, step 1 in registers, sub-step 0 operands of step 0 read
@@ -641,6 +676,12 @@ int launch_conv(const ConvArgs& a0, hipStream_t s) {
       return launch_status();
     }
   }
+  if constexpr (KH == 1 && KW == 1 && EPI == 0 && BN == 64 && TY == kTY) {  // the encoders' stem from the image
+    if (a.ain == kInImg) {
+      hipLaunchKernelGGL((conv_s32_kernel<KH, KW, BN, WM, WN, EPI, TY, kInImg>), grid, dim3(64 * WM * WN), 0, s, a);
+      return launch_status();
+    }
+  }
   if constexpr (KH == 1 && KW == 1 && EPI == 0 && BN == 128) {  // convc1 on the NHWC corr lookup
     if (a.ain == kInF32) {
       hipLaunchKernelGGL((conv_s32_kernel<KH, KW, BN, WM, WN, EPI, TY, kInF32>), grid, dim3(64 * WM * WN), 0, s, a);
@@ -802,7 +843,15 @@ extern "C" int oflow_conv_s32_ex3(const void* d_x, long long x_pixel_stride, int
                                  gru_channels, d_nhwc, nhwc_pixel_stride, d_stats, d_res, res_pixel_stride,
                                  res_activation, s2d);
   if (st != OFLOW_OK) return st;
-  if (in_format < kInS32 || in_format > kInF32) return OFLOW_E_MODE;
+  if (in_format < kInS32 || in_format > kInImg) return OFLOW_E_MODE;
+  if (in_format == kInImg) {  // the stem from the image: 1x1 geometry over 5 patch groups, BN 64, epilogue 0
+    if (kh != 1 || kw != 1 || epilogue != 0 || block_n != 64 || in_groups != (kImgK * kImgK * kImgC + 31) / 32)
+      return OFLOW_E_MODE;
+    if ((long long)kImgC * 4 * H * W >= (1ll << 31)) return OFLOW_E_SHAPE;
+    a.ain = in_format;
+    if (d_addend) return OFLOW_E_MODE;
+    return dispatch_conv(a, kh, kw, block_n, epilogue, static_cast<hipStream_t>(stream));
+  }
   if (in_format != kInF32 && (x_pixel_stride & 127)) return OFLOW_E_ALIGN;  // S32 / dense fp32: whole 128-B groups
   if (in_format == kInF32Norm && x_pixel_stride != (long long)in_groups * 128) return OFLOW_E_SHAPE;  // dense [P][kg*32]
   if (in_format == kInF32) {  // rows of cin fp32 channels, (kg - 1) * 32 < cin <= kg * 32, cin % 4 == 0

@@ -9,8 +9,9 @@
 //       thread, so no atomics. Coordinates get no gradient (the reference detaches coords1, raft.py:127).
 //   oflow_corr_pyramid_grad_combine_f32 : the levels' gradients folded into level 0 through the floor 2x2 average
 //       pools (corr.py:53): g0[q, y, x] += sum_l g_l[q, y >> l, x >> l] / 4^l where (y >> l, x >> l) is inside level l.
-// The two fmap gradients are then plain batched GEMMs (grad_f1 = f2 . g0^T / sqrt(C), grad_f2 = f1 . g0 / sqrt(C)),
-// left to rocBLAS through torch.bmm on the host side.
+//   oflow_corr_fmap_grad_f32 : the two fmap gradients, grad_f1 = f2 . g0^T / sqrt(C) and grad_f2 = f1 . g0 / sqrt(C)
+//       (the transpose of corr.py:85's matmul), as batched GEMMs on the fp32 matrix cores (v_mfma_f32_32x32x2_f32:
+//       exact fp32 fma chains, fixed k order per output: deterministic).
 #include "oflow_internal.h"
 
 namespace oflow {
@@ -110,6 +111,90 @@ __global__ __launch_bounds__(256) void pyramid_grad_combine_kernel2(float* __res
   }
 }
 
+// ---- fmap gradients: batched fp32 MFMA GEMM ----
+// C[b][m][n] = scale * sum_k A[b][m][k] * Bop[k][n], A row-major [M][K] (K contiguous: a feature map [C][N]); Bop = G^T
+// (TB: G [N][K] row-major, K contiguous) or G ([K][N] row-major, N contiguous). Workgroup tile 64 x 64, 4 waves as 2 x 2
+// of 32 x 32 (one v_mfma_f32_32x32x2_f32 accumulator each); K in chunks of 16 through LDS as [k][m] / [k][n] (the
+// MFMA reads lane l: A[m = l & 31][k = l >> 5], B[k = l >> 5][n = l & 31]: consecutive lanes, consecutive words);
+// global -> registers -> LDS one chunk ahead. Ragged M / N / K edges stage zeros.
+constexpr int kGT = 64, kGK = 16, kGThreads = 256;
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+template <bool TB>
+__global__ __launch_bounds__(kGThreads) void fmap_grad_gemm_kernel(const float* __restrict__ A, const float* __restrict__ G,
+                                                                   float* __restrict__ C, int M, int N, int K, float scale,
+                                                                   int tiles_n) {
+  __shared__ float sA[2][kGK][kGT + 4];
+  __shared__ float sB[2][kGK][kGT + 4];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+  const int b = blockIdx.y;
+  const int m0 = (blockIdx.x / tiles_n) * kGT, n0 = (blockIdx.x % tiles_n) * kGT;
+  const float* Ab = A + (size_t)b * M * K;
+  const float* Gb = G + (size_t)b * (size_t)N * K;  // G is [N][K] (TB) or [K][N]: N * K elements either way
+  // staging: A (and TB's G) as 64 rows x 16 k = 256 float4 along k; non-TB G as 16 k x 64 n = 256 float4 along n
+  const int ar = tid >> 2, ac4 = (tid & 3) * 4;
+  const int br = tid >> 4, bc4 = (tid & 15) * 4;
+  float4 ra, rb;
+  auto load = [&](int k0) {
+    float av[4], bv[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int k = k0 + ac4 + e;
+      av[e] = (m0 + ar < M && k < K) ? Ab[(size_t)(m0 + ar) * K + k] : 0.f;
+      if constexpr (TB) {
+        bv[e] = (n0 + ar < N && k < K) ? Gb[(size_t)(n0 + ar) * K + k] : 0.f;
+      } else {
+        const int n = n0 + bc4 + e, kk = k0 + br;
+        bv[e] = (n < N && kk < K) ? Gb[(size_t)kk * N + n] : 0.f;
+      }
+    }
+    ra = make_float4(av[0], av[1], av[2], av[3]);
+    rb = make_float4(bv[0], bv[1], bv[2], bv[3]);
+  };
+  auto store = [&](int buf) {
+    sA[buf][ac4 + 0][ar] = ra.x;
+    sA[buf][ac4 + 1][ar] = ra.y;
+    sA[buf][ac4 + 2][ar] = ra.z;
+    sA[buf][ac4 + 3][ar] = ra.w;
+    if constexpr (TB) {
+      sB[buf][ac4 + 0][ar] = rb.x;
+      sB[buf][ac4 + 1][ar] = rb.y;
+      sB[buf][ac4 + 2][ar] = rb.z;
+      sB[buf][ac4 + 3][ar] = rb.w;
+    } else {
+      *reinterpret_cast<float4*>(&sB[buf][br][bc4]) = rb;
+    }
+  };
+  f32x16 acc;
+#pragma unroll
+  for (int e = 0; e < 16; ++e) acc[e] = 0.f;
+  const int nk = (K + kGK - 1) / kGK;
+  load(0);
+  store(0);
+  __syncthreads();
+  for (int kc = 0; kc < nk; ++kc) {
+    const int buf = kc & 1;
+    if (kc + 1 < nk) load((kc + 1) * kGK);
+#pragma unroll
+    for (int kk = 0; kk < kGK; kk += 2) {
+      const float av = sA[buf][kk + (lane >> 5)][wm * 32 + (lane & 31)];
+      const float bv = sB[buf][kk + (lane >> 5)][wn * 32 + (lane & 31)];
+      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av, bv, acc, 0, 0, 0);
+    }
+    if (kc + 1 < nk) store(buf ^ 1);
+    __syncthreads();
+  }
+  // C/D map: acc[e] <-> row m = 4 * (lane >> 5) + (e & 3) + 8 * (e >> 2), column n = lane & 31
+  float* Cb = C + (size_t)b * M * N;
+  const int n = n0 + wn * 32 + (lane & 31);
+#pragma unroll
+  for (int e = 0; e < 16; ++e) {
+    const int m = m0 + wm * 32 + 4 * (lane >> 5) + (e & 3) + 8 * (e >> 2);
+    if (m < M && n < N) Cb[(size_t)m * N + n] = acc[e] * scale;
+  }
+}
+
 }  // namespace
 }  // namespace oflow
 
@@ -163,5 +248,20 @@ extern "C" int oflow_corr_pyramid_grad_combine_f32(float* const* d_grad_levels, 
   dim3 grid(static_cast<unsigned>(want < 1048576 ? want : 1048576));
   hipLaunchKernelGGL(pyramid_grad_combine_kernel2, grid, dim3(256), 0, static_cast<hipStream_t>(stream), d_grad_levels[0], t,
                      num_levels, Q, level_h[0], level_w[0]);
+  return launch_status();
+}
+
+extern "C" int oflow_corr_fmap_grad_f32(const float* d_fmap1, const float* d_fmap2, const float* d_g0, int B, int C, int N,
+                                        float scale, float* d_grad_f1, float* d_grad_f2, void* stream) {
+  if (!d_fmap1 || !d_fmap2 || !d_g0 || (!d_grad_f1 && !d_grad_f2)) return OFLOW_E_NULL;
+  if (B < 0 || C <= 0 || N < 0) return OFLOW_E_SHAPE;
+  if (B == 0 || N == 0) return OFLOW_OK;
+  if ((long long)N * N >= (1ll << 40) || B > 65535) return OFLOW_E_SHAPE;
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  const int tm = (C + kGT - 1) / kGT, tn = (N + kGT - 1) / kGT;
+  const dim3 grid(tm * tn, B);
+  // grad_f1[c][q] = scale * sum_t f2[c][t] g0[q][t]; grad_f2[c][t] = scale * sum_q f1[c][q] g0[q][t]
+  if (d_grad_f1) hipLaunchKernelGGL((fmap_grad_gemm_kernel<true>), grid, dim3(kGThreads), 0, s, d_fmap2, d_g0, d_grad_f1, C, N, N, scale, tn);
+  if (d_grad_f2) hipLaunchKernelGGL((fmap_grad_gemm_kernel<false>), grid, dim3(kGThreads), 0, s, d_fmap1, d_g0, d_grad_f2, C, N, N, scale, tn);
   return launch_status();
 }

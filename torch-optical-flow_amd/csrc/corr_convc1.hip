@@ -120,34 +120,37 @@ __global__ __launch_bounds__(kNT, 2) void corr_convc1_kernel(C1Args a) {
     for (int j = 1; j < OFLOW_MAX_LEVELS; ++j)
       if (j == l) { Hl = a.Hl[j]; Wl = a.Wl[j]; WB = a.WB[j]; LF = a.LF[j]; base = a.lv[j]; }
   };
-  // window of query tid at level l -> sO / sW[l & 3] (threads < kQM)
+  const int qd = tid & (kQM - 1);            // the query a decoding thread handles
+  const bool dwave = tid >= (kNT - kQM);      // wave 3: decodes levels 2.. inside the loop
+  // window of query qd at level l -> sO / sW[l & 3]
   auto decode = [&](int l, float cx, float cy) {
     int Hl, Wl, WB, LF;
     const float* base;
     level(l, Hl, Wl, WB, LF, base);
     int xs, ys;
     float4 w4;
-    window_origin(cx, cy, 1.0f / static_cast<float>(1 << l), R, xs, ys, w4);  // 1/2^l exact (corr.py:68)
+    window_origin(cx, cy, __int_as_float((127 - l) << 23), R, xs, ys, w4);  // 1/2^l exactly (corr.py:68)
     const int dx = xs & 3, xa = xs - dx;
     const int xl = max(0, -xa), xh = min(4 * NCH, Wl - xa);
     const int yl = max(0, -ys), yh = min(PK, Hl - ys);
     const unsigned xm = xh > xl ? (((1u << (xh - xl)) - 1u) << xl) : 0u;
     const unsigned ym = yh > yl ? (((1u << (yh - yl)) - 1u) << yl) : 0u;
-    sO[l & (NS - 1)][tid] = make_int4(xs, ys, static_cast<int>(xm | (ym << 16)), dx);
-    sW[l & (NS - 1)][tid] = w4;
+    sO[l & (NS - 1)][qd] = make_int4(xs, ys, static_cast<int>(xm | (ym << 16)), dx);
+    sW[l & (NS - 1)][qd] = w4;
   };
 
   for (int c = tid; c < kN; c += kNT) sSB[c] = make_float2(a.wsc[c], a.bias ? a.bias[c] : 0.f);
-  if (tid < kQM) {
+  // the query's coordinates; waves 0 and 1 decode levels 0 and 1 (wave 3, the one with the fewest tap slots, decodes
+  // the later levels inside the loop)
+  if (wave < 2) {
     float2 c = make_float2(1e30f, 1e30f);  // past the last query: all-zero window
-    if (tid < nq) {
-      const int q = q0 + tid;
+    if (qd < nq) {
+      const int q = q0 + qd;
       const int b = q / a.N, pix = q - b * a.N;
       c = make_float2(a.coords[(size_t)(2 * b) * a.N + pix], a.coords[(size_t)(2 * b + 1) * a.N + pix]);
     }
-    sC[tid] = c;
-    decode(0, c.x, c.y);
-    if (a.nlev > 1) decode(1, c.x, c.y);
+    if (wave == 0) sC[qd] = c;
+    if (wave < a.nlev) decode(wave, c.x, c.y);
   }
   // A's taps past KK (the last group's tail) are never written again: zero the whole A buffer once
   for (int e = tid; e < A_BYTES / 16; e += kNT) reinterpret_cast<u32x4*>(sA)[e] = u32x4{0u, 0u, 0u, 0u};
@@ -240,7 +243,7 @@ __global__ __launch_bounds__(kNT, 2) void corr_convc1_kernel(C1Args a) {
     stamp();
     // ---- 2. next level's gathers (rv is free), the level after next's windows ----
     if (l + 1 < a.nlev) gather(l + 1);
-    if (tid < kQM && l + 2 < a.nlev) decode(l + 2, sC[tid].x, sC[tid].y);
+    if (dwave && l + 2 < a.nlev) decode(l + 2, sC[qd].x, sC[qd].y);
     // ---- 3. bilinear taps -> split-fp16 A operand; the slot set is the wave index (a scalar branch per slot) ----
     {
       const int q = tid & (kQM - 1), set = __builtin_amdgcn_readfirstlane(tid / kQM);

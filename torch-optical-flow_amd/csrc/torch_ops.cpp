@@ -16,7 +16,9 @@
 //   grid_warp(frame, flow, mode, padding_mode, align_corners)     optical_flow.warp   (operator.py:8-33)
 //   grid_sample(input, grid, mode, padding_mode, align_corners)   bilinear_sampler    (utils.py:64-80)
 //   corr_lookup_backward(grad_out, coords, radius, H0, W0, L)     transpose of corr_lookup (training, §8(f) row 3)
-//   corr_pyramid_backward(level_grads, fmap1, fmap2) -> (g1, g2)  pool transpose + two batched GEMMs
+//   corr_pyramid_backward(level_grads, fmap1, fmap2) -> (g1, g2)  pool transpose + two fp32-MFMA GEMMs
+//   grid_warp_backward(grad_out, frame, flow, mode, pad, ac) -> (grad_frame, grad_flow)     warp's autograd
+//   grid_sample_backward(grad_out, input, grid, mode, pad, ac) -> (grad_input, grad_grid)   grid_sample's autograd
 #include <torch/library.h>
 #include <ATen/ATen.h>
 #include <ATen/hip/HIPContext.h>
@@ -393,6 +395,58 @@ Tensor grid_sample_meta(const Tensor& input, const Tensor& grid, int64_t mode, i
   return at::empty({input.size(0), input.size(1), grid.size(1), grid.size(2)}, input.options().dtype(at::kFloat));
 }
 
+// warp / grid_sample backward (warp_backward.hip): (grad_frame, grad_flow) / (grad_input, grad_grid)
+std::tuple<Tensor, Tensor> grid_warp_backward_impl(const Tensor& gout, const Tensor& frame, const Tensor& flow,
+                                                   int64_t mode, int64_t pad, bool ac, bool run) {
+  const char* what = "warp backward";
+  check_modes(mode, pad, what);
+  check_warp(frame, flow, what);
+  TORCH_CHECK(gout.sizes() == frame.sizes(), what, ": grad_out ", gout.sizes(), " must match the frame ", frame.sizes());
+  if (!run) return {at::empty(frame.sizes(), frame.options().dtype(at::kFloat)), at::empty(flow.sizes(), flow.options().dtype(at::kFloat))};
+  Tensor go = gpu_f32(gout, "grad_out", what), fr = gpu_f32(frame, "frame", what), fl = gpu_f32(flow, "flow", what);
+  Tensor gfr = at::zeros_like(fr), gfl = at::empty_like(fl);
+  if (fr.numel() == 0) return {gfr, gfl.zero_()};
+  c10::hip::HIPGuardMasqueradingAsCUDA g(fr.device());
+  check_status(oflow_grid_warp_backward_f32(go.data_ptr<float>(), fr.data_ptr<float>(), fl.data_ptr<float>(), (int)fr.size(0),
+                                            (int)fr.size(1), (int)fr.size(2), (int)fr.size(3), (int)mode, (int)pad, ac ? 1 : 0,
+                                            gfr.data_ptr<float>(), gfl.data_ptr<float>(), cur_stream()),
+               what);
+  return {gfr, gfl};
+}
+std::tuple<Tensor, Tensor> grid_warp_backward_hip(const Tensor& go, const Tensor& fr, const Tensor& fl, int64_t m, int64_t p, bool ac) {
+  return grid_warp_backward_impl(go, fr, fl, m, p, ac, true);
+}
+std::tuple<Tensor, Tensor> grid_warp_backward_meta(const Tensor& go, const Tensor& fr, const Tensor& fl, int64_t m, int64_t p, bool ac) {
+  return grid_warp_backward_impl(go, fr, fl, m, p, ac, false);
+}
+
+std::tuple<Tensor, Tensor> grid_sample_backward_impl(const Tensor& gout, const Tensor& input, const Tensor& grid,
+                                                     int64_t mode, int64_t pad, bool ac, bool run) {
+  const char* what = "grid_sample backward";
+  check_modes(mode, pad, what);
+  check_sample(input, grid, what);
+  TORCH_CHECK(gout.dim() == 4 && gout.size(0) == input.size(0) && gout.size(1) == input.size(1) &&
+                  gout.size(2) == grid.size(1) && gout.size(3) == grid.size(2),
+              what, ": grad_out ", gout.sizes(), " must be (B, C, Ho, Wo)");
+  if (!run) return {at::empty(input.sizes(), input.options().dtype(at::kFloat)), at::empty(grid.sizes(), grid.options().dtype(at::kFloat))};
+  Tensor go = gpu_f32(gout, "grad_out", what), x = gpu_f32(input, "input", what), gr = gpu_f32(grid, "grid", what);
+  Tensor gx = at::zeros_like(x), gg = at::empty_like(gr);
+  if (go.numel() == 0) return {gx, gg.zero_()};
+  c10::hip::HIPGuardMasqueradingAsCUDA g(x.device());
+  check_status(oflow_grid_sample_backward_f32(go.data_ptr<float>(), x.data_ptr<float>(), gr.data_ptr<float>(), (int)x.size(0),
+                                              (int)x.size(1), (int)x.size(2), (int)x.size(3), (int)gr.size(1), (int)gr.size(2),
+                                              (int)mode, (int)pad, ac ? 1 : 0, gx.data_ptr<float>(), gg.data_ptr<float>(),
+                                              cur_stream()),
+               what);
+  return {gx, gg};
+}
+std::tuple<Tensor, Tensor> grid_sample_backward_hip(const Tensor& go, const Tensor& x, const Tensor& gr, int64_t m, int64_t p, bool ac) {
+  return grid_sample_backward_impl(go, x, gr, m, p, ac, true);
+}
+std::tuple<Tensor, Tensor> grid_sample_backward_meta(const Tensor& go, const Tensor& x, const Tensor& gr, int64_t m, int64_t p, bool ac) {
+  return grid_sample_backward_impl(go, x, gr, m, p, ac, false);
+}
+
 // ---------------------------------------------------------------- backward (training path, §8(f) row 3)
 std::vector<Tensor> lookup_backward_impl(const Tensor& grad_out, const Tensor& coords, int64_t radius, int64_t h0,
                                          int64_t w0, int64_t nl, bool run) {
@@ -463,11 +517,13 @@ std::tuple<Tensor, Tensor> pyramid_backward_impl(const std::vector<Tensor>& leve
     }
     check_status(oflow_corr_pyramid_grad_combine_f32(ptrs, hs, ws, (int)nl, b * n, cur_stream()), what);
   }
-  Tensor g0 = gl[0].view({b, n, n});
-  const double s = 1.0 / std::sqrt((double)c);
-  Tensor f1m = fmap1.to(at::kFloat).reshape({b, c, n}), f2m = fmap2.to(at::kFloat).reshape({b, c, n});
-  Tensor g1 = at::bmm(f2m, g0.transpose(1, 2)).mul_(s).view({b, c, h, w});
-  Tensor g2 = at::bmm(f1m, g0).mul_(s).view({b, c, h, w});
+  // the fmap gradients on the fp32 matrix cores (corr_backward.hip): scale as the forward, 1/sqrt(float(C))
+  const float s = 1.0f / std::sqrt(static_cast<float>(c));
+  Tensor f1m = fmap1.to(at::kFloat).contiguous(), f2m = fmap2.to(at::kFloat).contiguous();
+  Tensor g1 = at::empty({b, c, h, w}, f1m.options()), g2 = at::empty({b, c, h, w}, f2m.options());
+  check_status(oflow_corr_fmap_grad_f32(f1m.data_ptr<float>(), f2m.data_ptr<float>(), gl[0].data_ptr<float>(), (int)b,
+                                        (int)c, (int)n, s, g1.data_ptr<float>(), g2.data_ptr<float>(), cur_stream()),
+               what);
   return {g1.to(fmap1.scalar_type()), g2.to(fmap2.scalar_type())};
 }
 
@@ -492,6 +548,8 @@ TORCH_LIBRARY(oflow, m) {
   m.def("grid_sample(Tensor input, Tensor grid, int mode, int padding_mode, bool align_corners) -> Tensor");
   m.def("corr_lookup_backward(Tensor grad_out, Tensor coords, int radius, int H, int W, int num_levels) -> Tensor[]");
   m.def("corr_pyramid_backward(Tensor[] level_grads, Tensor fmap1, Tensor fmap2) -> (Tensor, Tensor)");
+  m.def("grid_warp_backward(Tensor grad_out, Tensor frame, Tensor flow, int mode, int padding_mode, bool align_corners) -> (Tensor, Tensor)");
+  m.def("grid_sample_backward(Tensor grad_out, Tensor input, Tensor grid, int mode, int padding_mode, bool align_corners) -> (Tensor, Tensor)");
 }
 
 TORCH_LIBRARY_IMPL(oflow, CUDA, m) {
@@ -506,6 +564,8 @@ TORCH_LIBRARY_IMPL(oflow, CUDA, m) {
   m.impl("grid_sample", &grid_sample_hip);
   m.impl("corr_lookup_backward", &lookup_backward_hip);
   m.impl("corr_pyramid_backward", &pyramid_backward_hip);
+  m.impl("grid_warp_backward", &grid_warp_backward_hip);
+  m.impl("grid_sample_backward", &grid_sample_backward_hip);
 }
 
 // CPU tensors reach the same kernels, whose first check raises "no CPU fallback" (there is no CPU path)
@@ -521,6 +581,8 @@ TORCH_LIBRARY_IMPL(oflow, CPU, m) {
   m.impl("grid_sample", &grid_sample_hip);
   m.impl("corr_lookup_backward", &lookup_backward_hip);
   m.impl("corr_pyramid_backward", &pyramid_backward_hip);
+  m.impl("grid_warp_backward", &grid_warp_backward_hip);
+  m.impl("grid_sample_backward", &grid_sample_backward_hip);
 }
 
 TORCH_LIBRARY_IMPL(oflow, Meta, m) {
@@ -535,4 +597,6 @@ TORCH_LIBRARY_IMPL(oflow, Meta, m) {
   m.impl("grid_sample", &grid_sample_meta);
   m.impl("corr_lookup_backward", &lookup_backward_meta);
   m.impl("corr_pyramid_backward", &pyramid_backward_meta);
+  m.impl("grid_warp_backward", &grid_warp_backward_meta);
+  m.impl("grid_sample_backward", &grid_sample_backward_meta);
 }

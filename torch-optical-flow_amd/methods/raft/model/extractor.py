@@ -234,11 +234,13 @@ class SplitEncoder:
         return patches
 
     def __call__(self, x: Union[Tensor, Sequence[Tensor]], patches: Optional[Tensor] = None,
-                 split_out: bool = False) -> Union[Tensor, Tuple[Tensor, ...]]:
+                 split_out: bool = False, stem_from_image: bool = False) -> Union[Tensor, Tuple[Tensor, ...]]:
         """``patches``: the stem's patch matrix of ``x`` when another encoder already built it (RAFT's cnet reads
         image0's rows of fnet's, raft.py:109/115); the one built here is kept as ``self.patches``. ``split_out``: the
         head convolution writes its output as S32 rows (B, H, W, C/32, 2, 32) instead of fp32 NCHW (the RAFT forward's
-        correlation input, CorrBlock.from_split_features)."""
+        correlation input, CorrBlock.from_split_features). ``stem_from_image``: the stem convolution builds its 7x7
+        patch operand from the image tile by tile (OFLOW_IN_IMG7S2) instead of reading a patch matrix (none is
+        written; ``patches`` is ignored)."""
         is_list = isinstance(x, (tuple, list))
         if is_list:
             batch_dim = x[0].shape[0]
@@ -256,14 +258,21 @@ class SplitEncoder:
             raise RuntimeError("SplitEncoder: H and W must be multiples of 8")
         V = _native.S32Slice
         h, w = hh // 2, ww // 2
-        if patches is None or tuple(patches.shape[:4]) != (n, h, w, self.w["stem"].kg):
-            patches = _native.s32_empty(n, h, w, self.w["stem"].kg, dev)
-            _native.stem_patches(x, patches)
-        self.patches = patches
+        if stem_from_image:
+            if isinstance(x, (tuple, list)):
+                x = torch.cat([t.float() for t in x], dim=0)
+            stem_in = _native.ImgIn(x.float().contiguous())
+            self.patches = None
+        else:
+            if patches is None or tuple(patches.shape[:4]) != (n, h, w, self.w["stem"].kg):
+                patches = _native.s32_empty(n, h, w, self.w["stem"].kg, dev)
+                _native.stem_patches(x, patches)
+            self.patches = patches
+            stem_in = V(patches)
         # instance norm: the stem's output stays raw fp32 + its norm (relu(norm(.)) applied by layer1's first conv while
         # it stages its input, and by that block's residual tail): no normalised copy is written
-        cur = (self._conv1(V(patches), self.w["stem"], (n, h, w)) if self.inorm
-               else self._conv_norm(V(patches), self.w["stem"], (n, h, w), "relu"))
+        cur = (self._conv1(stem_in, self.w["stem"], (n, h, w)) if self.inorm
+               else self._conv_norm(stem_in, self.w["stem"], (n, h, w), "relu"))
         layers = (self.enc.layer1, self.enc.layer2, self.enc.layer3)
         for li, layer in enumerate(layers):
             for bi, blk in enumerate(layer):

@@ -109,6 +109,9 @@ class RAFT(nn.Module):
         # with the split encoders, fnet writes its features as S32 rows and the pyramid is built from split-fp16
         # products (oflow_corr_pyramid_tiled_s32); False: fp32 features and the fp32-MFMA pyramid
         self.split_corr = True
+        # split encoders: the stem convolution builds its 7x7 patch operand from the image tile by tile
+        # (OFLOW_IN_IMG7S2) instead of reading a patch matrix written beforehand (fnet's image0 rows shared with cnet)
+        self.stem_from_image = True
         # the split paths cache packed fp16 hi/lo weights keyed by (storage, version); parameters created under
         # torch.inference_mode() have no version counter, so loading new weights in place drops the caches
         for m in (self.fnet, self.cnet, self.update_block):
@@ -253,34 +256,36 @@ class RAFT(nn.Module):
             nb = image0.shape[0]
             side2 = (_side_stream(image0.device, 1) if side is not None and self.fnet_streams
                      and block is CorrBlock and self.split_corr else None)
+            sfi = self.stem_from_image
             if side2 is not None:
-                # fnet's two images on two streams, each building its own stem patches (instance norm is per image:
-                # the same values as one batch), so three 8-image encoders share the chip and finish together
+                # fnet's two images on two streams (instance norm is per image: the same values as one batch), so
+                # three 8-image encoders share the chip and finish together
                 side2.wait_stream(main)
                 with torch.cuda.stream(side2):
-                    f2s = fnet(image1, split_out=True)
-                patches = fnet.stem_patches(image0)
+                    f2s = fnet(image1, split_out=True, stem_from_image=sfi)
+                patches = None if sfi else fnet.stem_patches(image0)
             else:
-                patches = fnet.stem_patches(torch.cat([image0, image1], dim=0))
+                patches = None if sfi else fnet.stem_patches(torch.cat([image0, image1], dim=0))
+            cpatches = None if patches is None else patches[:nb]
             if side is not None:
                 side.wait_stream(main)
                 with torch.cuda.stream(side):
-                    cnet_out = cnet(image0, patches=patches[:nb])
+                    cnet_out = cnet(image0, patches=cpatches, stem_from_image=sfi)
             if block is CorrBlock and self.split_corr:
                 # features as S32 rows straight from fnet's head conv -> split-fp16 pyramid (no fp32 fmaps)
                 if side2 is not None:
-                    f1s = fnet(image0, patches=patches, split_out=True)
+                    f1s = fnet(image0, patches=patches, split_out=True, stem_from_image=sfi)
                     main.wait_stream(side2)
                 else:
-                    f1s, f2s = fnet([image0, image1], patches=patches, split_out=True)
+                    f1s, f2s = fnet([image0, image1], patches=patches, split_out=True, stem_from_image=sfi)
                 corr_fn = CorrBlock.from_split_features(f1s, f2s, radius=self.hparams.corr_radius)
             else:
-                fmap1, fmap2 = fnet([image0, image1], patches=patches)
+                fmap1, fmap2 = fnet([image0, image1], patches=patches, stem_from_image=sfi)
                 corr_fn = block(fmap1.float(), fmap2.float(), radius=self.hparams.corr_radius)
             if side is not None:
                 main.wait_stream(side)
             else:
-                cnet_out = cnet(image0, patches=patches[: image0.shape[0]])
+                cnet_out = cnet(image0, patches=cpatches, stem_from_image=sfi)
         else:
             fmap1, fmap2 = fnet([image0, image1])
             corr_fn = block(fmap1.float(), fmap2.float(), radius=self.hparams.corr_radius)

@@ -68,6 +68,9 @@ SYMBOLS = (
     "oflow_corr_pyramid_tiled_s32",
     "oflow_flow_head2_s32",
     "oflow_conv_s32_ex3",
+    "oflow_corr_fmap_grad_f32",
+    "oflow_grid_warp_backward_f32",
+    "oflow_grid_sample_backward_f32",
 )
 
 _lib = None
@@ -630,6 +633,39 @@ class F32In:
     @property
     def ng(self) -> int:
         return (int(self.raw.shape[1]) + 31) // 32
+
+    @property
+    def device(self):
+        return self.raw.device
+
+
+class ImgIn:
+    """The encoders' stem input given as the fp32 NCHW image (B, 3, 2H, 2W) itself (OFLOW_IN_IMG7S2): the 7x7/2 pad-3
+    conv's patch operand is built per output tile from the staged input window, so no patch matrix is written. For
+    ConvWeights packed with ``patches=True`` (5 groups); the output is (B, H, W)."""
+
+    __slots__ = ("raw", "bhw")
+    in_format = 3
+
+    def __init__(self, img: torch.Tensor):
+        if img.dtype != torch.float32 or img.dim() != 4 or img.shape[1] != 3 or not img.is_contiguous():
+            raise RuntimeError("ImgIn: the image must be contiguous fp32 (B, 3, H, W)")
+        b, _, hh, ww = img.shape
+        if hh % 2 or ww % 2:
+            raise RuntimeError("ImgIn: H and W must be even")
+        self.raw, self.bhw = img, (int(b), int(hh) // 2, int(ww) // 2)
+
+    @property
+    def ptr(self) -> int:
+        return self.raw.data_ptr()
+
+    @property
+    def ps(self) -> int:
+        return 0
+
+    @property
+    def ng(self) -> int:
+        return 5
 
     @property
     def device(self):

@@ -7,11 +7,12 @@ registers the autograd formulas on top, so ``CorrBlock`` and ``optical_flow.warp
 
 Autograd:
   * ``corr_pyramid``: the level gradients go back through the floor 2x2 pools (native kernel) and two batched GEMMs
-    (``corr_pyramid_backward``): grad_f1 = f2 . G^T / sqrt(C), grad_f2 = f1 . G / sqrt(C).
+    (``corr_pyramid_backward``, fp32 MFMA): grad_f1 = f2 . G^T / sqrt(C), grad_f2 = f1 . G / sqrt(C).
   * ``corr_lookup``: the native transpose of the bilinear window gather (``corr_lookup_backward``); coords get no
     gradient -- the reference detaches them before every lookup (methods/raft/model/raft.py:127).
-  * ``grid_warp`` / ``grid_sample``: ATen's grid_sampler_2d_backward on the same grid (frame and flow / grid
-    gradients); the warp's base grid is constant, so the flow gradient is the grid gradient.
+  * ``grid_warp`` / ``grid_sample``: the native transpose (``grid_warp_backward`` / ``grid_sample_backward``,
+    csrc/warp_backward.hip: ATen grid_sampler_2d_backward's formulas, tap gradients added with fp32 atomics); the
+    warp's base grid is constant, so the flow gradient is the grid gradient.
 The tiled / NHWC / fp16 on-the-fly lookups are the inference layouts and have no autograd formula.
 """
 from __future__ import annotations
@@ -35,6 +36,8 @@ OPS = (
     "grid_sample",
     "corr_lookup_backward",
     "corr_pyramid_backward",
+    "grid_warp_backward",
+    "grid_sample_backward",
 )
 _loaded = False
 
@@ -99,14 +102,6 @@ def _lookup_backward(ctx, grad_out):
     return list(grads), None, None
 
 
-def _base_grid(b: int, h: int, w: int, device) -> torch.Tensor:
-    """The reference warp's linspace(-1, 1) base grid (B, H, W, 2) (operator.py:36-56)."""
-    gy, gx = torch.meshgrid(
-        torch.linspace(-1.0, 1.0, h, device=device), torch.linspace(-1.0, 1.0, w, device=device), indexing="ij"
-    )
-    return torch.stack((gx, gy), dim=-1).unsqueeze(0).expand(b, h, w, 2)
-
-
 def _warp_setup(ctx, inputs, output):
     frame, flow, mode, pad, ac = inputs
     ctx.save_for_backward(frame, flow)
@@ -116,13 +111,10 @@ def _warp_setup(ctx, inputs, output):
 def _warp_backward(ctx, grad_out):
     frame, flow = ctx.saved_tensors
     mode, pad, ac = ctx.args
-    b, _, h, w = flow.shape
-    grid = _base_grid(b, h, w, flow.device) + flow.float().permute(0, 2, 3, 1)
-    g_in, g_grid = torch.ops.aten.grid_sampler_2d_backward(
-        grad_out.contiguous(), frame.float(), grid, mode, pad, ac, [ctx.needs_input_grad[0], ctx.needs_input_grad[1]]
-    )
+    # the native transpose (warp_backward.hip): grid = linspace base + flow, so the flow gradient is the grid gradient
+    g_in, g_flow = torch.ops.oflow.grid_warp_backward(grad_out.contiguous(), frame, flow, mode, pad, ac)
     g_frame = g_in.to(frame.dtype) if ctx.needs_input_grad[0] else None
-    g_flow = g_grid.permute(0, 3, 1, 2).to(flow.dtype) if ctx.needs_input_grad[1] else None
+    g_flow = g_flow.to(flow.dtype) if ctx.needs_input_grad[1] else None
     return g_frame, g_flow, None, None, None
 
 
@@ -135,9 +127,7 @@ def _sample_setup(ctx, inputs, output):
 def _sample_backward(ctx, grad_out):
     inp, grid = ctx.saved_tensors
     mode, pad, ac = ctx.args
-    g_in, g_grid = torch.ops.aten.grid_sampler_2d_backward(
-        grad_out.contiguous(), inp.float(), grid.float(), mode, pad, ac, [ctx.needs_input_grad[0], ctx.needs_input_grad[1]]
-    )
+    g_in, g_grid = torch.ops.oflow.grid_sample_backward(grad_out.contiguous(), inp, grid, mode, pad, ac)
     g_x = g_in.to(inp.dtype) if ctx.needs_input_grad[0] else None
     g_g = g_grid.to(grid.dtype) if ctx.needs_input_grad[1] else None
     return g_x, g_g, None, None, None
