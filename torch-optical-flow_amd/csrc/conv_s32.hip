@@ -160,8 +160,11 @@ __global__ __launch_bounds__(64 * WM * WN, WM * WN == 8 ? 1 : 2) void conv_s32_k
   constexpr int TS = BN + 4;              // epilogue tile row stride (floats)
   constexpr int EPI_BYTES = BM * TS * 4;
   constexpr int LDS_BYTES = MAIN_BYTES > EPI_BYTES ? MAIN_BYTES : EPI_BYTES;
-  constexpr int AFF_BYTES = AIN == kInF32Norm ? kAinGroups * 32 * 8       // float2 (scale, shift) per input channel
-                            : AIN == kInImg ? kImgC * kImgRows * kImgCols * 4  // the stem's input window
+  // kInImg: the stem's input window [c][row][col] + one zero float, then the patch channels' window offsets
+  constexpr int kImgZero = kImgC * kImgRows * kImgCols;
+  constexpr int IMG_FLOATS = (kImgZero + 1 + 3) & ~3;
+  constexpr int AFF_BYTES = AIN == kInF32Norm ? kAinGroups * 32 * 8  // float2 (scale, shift) per input channel
+                            : AIN == kInImg ? IMG_FLOATS * 4 + 160 * 4
                             : 0;
   static_assert(AIN != kInImg || (T == 1 && TY == kTY), "image input: 1x1 geometry over the patch channels, 4-row tiles");
   __shared__ __attribute__((aligned(16))) uint8_t smem[LDS_BYTES + AFF_BYTES];
@@ -169,7 +172,8 @@ __global__ __launch_bounds__(64 * WM * WN, WM * WN == 8 ? 1 : 2) void conv_s32_k
   // wait on a global-load round trip per iteration)
   __shared__ float2 sSB[BN];
   float2* sAff = reinterpret_cast<float2*>(smem + LDS_BYTES);
-  float* sImg = reinterpret_cast<float*>(smem + LDS_BYTES);  // kInImg: [c][row][col]
+  float* sImg = reinterpret_cast<float*>(smem + LDS_BYTES);  // kInImg: [c][row][col], zero at kImgZero
+  int* sKoff = reinterpret_cast<int*>(smem + LDS_BYTES + (AIN == kInImg ? IMG_FLOATS * 4 : 0));
   uint8_t* sA = smem;
   uint8_t* sB = smem + (ADB ? 2 : 1) * A_BYTES;
 
@@ -241,14 +245,12 @@ __global__ __launch_bounds__(64 * WM * WN, WM * WN == 8 ? 1 : 2) void conv_s32_k
         typedef _Float16 half4_ __attribute__((ext_vector_type(4)));                                                 \
         half4_ h4 = {0, 0, 0, 0}, l4 = {0, 0, 0, 0};                                                                 \
         if constexpr (AIN == kInImg) {                                                                               \
-          /* patch channel k = t*3 + ch, t = ky*7 + kx, of pixel p: the staged window at (2*py + ky, 2*px + kx) */   \
-          const int py_ = p / kTX, px_ = p - py_ * kTX;                                                              \
+          /* patch channel k of pixel p = the staged window at (2*py, 2*px) + the channel's table offset */          \
+          const int pb_ = 2 * (p >> 5) * kImgCols + 2 * (p & 31);                                                    \
+          const int4 ko_ = *reinterpret_cast<const int4*>(sKoff + (G) * 32 + 4 * c);                                 \
+          const int kov_[4] = {ko_.x, ko_.y, ko_.z, ko_.w};                                                          \
           _Pragma("unroll") for (int e_ = 0; e_ < 4; ++e_) {                                                         \
-            const int k_ = (G) * 32 + 4 * c + e_;                                                                    \
-            const int t_ = k_ / kImgC, ch_ = k_ - t_ * kImgC;                                                        \
-            const int ky_ = t_ / kImgK, kx_ = t_ - ky_ * kImgK;                                                      \
-            const float v_ = t_ < kImgK * kImgK                                                                      \
-                ? sImg[(ch_ * kImgRows + 2 * py_ + ky_) * kImgCols + 2 * px_ + kx_] : 0.f;                           \
+            const float v_ = sImg[kov_[e_] < 0 ? kImgZero : pb_ + kov_[e_]];                                         \
             _Float16 hv, lv;                                                                                         \
             split_f16(v_, hv, lv);                                                                                   \
             h4[e_] = hv;                                                                                             \
@@ -353,6 +355,12 @@ __global__ __launch_bounds__(64 * WM * WN, WM * WN == 8 ? 1 : 2) void conv_s32_k
         v = img[((long long)ch * (2 * a.H) + iy) * (2 * a.W) + ix];
       sImg[e] = v;
     }
+    // patch channel k = t*3 + ch, t = ky*7 + kx -> window offset ch*(rows*cols) + ky*cols + kx (-1: zero, k >= 147)
+    for (int k = tid; k < 160; k += NTH) {
+      const int t = k / kImgC, ch = k - t * kImgC;
+      sKoff[k] = t < kImgK * kImgK ? (ch * kImgRows + t / kImgK) * kImgCols + t % kImgK : -1;
+    }
+    if (tid == 0) sImg[kImgZero] = 0.f;
     __syncthreads();
   }
   // prologue: step 0 in LDS, step 1 in registers, sub-step 0 operands of step 0 read

@@ -14,6 +14,8 @@
 // Bilinear (the default mode): warp_bilinear_lds_kernel stages each 16 x 64 output tile's source box in LDS (below).
 // Other modes, and frames whose rows are not 16-B multiples: one thread per output pixel, flow read and output
 // writes coalesced along W; the gathered taps of neighbouring lanes are neighbours too for smooth flow.
+#include <algorithm>
+
 #include "oflow_internal.h"
 
 #pragma clang fp contract(off)
@@ -208,7 +210,7 @@ constexpr int kBoxFloats = 9216;  // 36 KB (4 workgroups per CU): a 16 x 64 tile
 constexpr int kWChunks = kBoxFloats / 4 / kWThreads;  // 16-B box chunks per thread (12)
 
 template <bool FLOW>
-__global__ __launch_bounds__(kWThreads) void warp_bilinear_lds_kernel(WarpArgs a, int tiles_x, int tiles_y) {
+__global__ __launch_bounds__(kWThreads) void warp_bilinear_lds_kernel(WarpArgs a, int tiles_x, int tiles_y, int cpw) {
   __shared__ __attribute__((aligned(16))) float sBox[kBoxFloats];
   __shared__ int sRed[kWWaves][4];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -217,6 +219,10 @@ __global__ __launch_bounds__(kWThreads) void warp_bilinear_lds_kernel(WarpArgs a
   // staged boxes overlap most (speed only; the remap is a bijection for any grid size)
   const int nwg = gridDim.x, q8 = nwg / 8, r8 = nwg % 8, xcd = blockIdx.x % 8;
   int t = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + blockIdx.x / 8;
+  // channel chunks of one tile are consecutive in that order (one XCD: the flow is read from HBM once)
+  const int nch = (a.C + cpw - 1) / cpw;
+  const int cb = (t % nch) * cpw, ce = min(a.C, cb + cpw);
+  t /= nch;
   const int ty = t % tiles_y;
   t /= tiles_y;
   const int tx = t % tiles_x;
@@ -305,6 +311,7 @@ __global__ __launch_bounds__(kWThreads) void warp_bilinear_lds_kernel(WarpArgs a
 
   if (!staged) {
     // direct gathers, pixel-major: 4 channels' 16 taps of a pixel in flight before any store (grid_warp_kernel's loop)
+    // (this workgroup's channel chunk [cb, ce))
 #pragma unroll
     for (int k = 0; k < kWRows; ++k) {
       if (!((vmask >> (16 + k)) & 1u)) continue;
@@ -313,12 +320,12 @@ __global__ __launch_bounds__(kWThreads) void warp_bilinear_lds_kernel(WarpArgs a
       const int y0 = static_cast<int>(static_cast<short>(o00[k] & 0xffff)), x0 = o00[k] >> 16;
       const int o = y0 * a.W + x0;
       float* __restrict__ d = dst + yo * a.Wo + xo;
-      for (int c0 = 0; c0 < a.C; c0 += 4) {
+      for (int c0 = cb; c0 < ce; c0 += 4) {
         float v[4][4];
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
           const float* sp = src + (size_t)(c0 + q) * HW + o;
-          const bool ok = c0 + q < a.C;
+          const bool ok = c0 + q < ce;
           v[q][0] = (ok && (m & 1u)) ? sp[0] : 0.0f;
           v[q][1] = (ok && (m & 2u)) ? sp[1] : 0.0f;
           v[q][2] = (ok && (m & 4u)) ? sp[a.W] : 0.0f;
@@ -326,7 +333,7 @@ __global__ __launch_bounds__(kWThreads) void warp_bilinear_lds_kernel(WarpArgs a
         }
 #pragma unroll
         for (int q = 0; q < 4; ++q)
-          if (c0 + q < a.C) d[(size_t)(c0 + q) * HWo] = bilerp(v[q], wnw[k], wne[k], wsw[k], wse[k]);
+          if (c0 + q < ce) d[(size_t)(c0 + q) * HWo] = bilerp(v[q], wnw[k], wne[k], wsw[k], wse[k]);
       }
     }
     return;
@@ -359,12 +366,12 @@ __global__ __launch_bounds__(kWThreads) void warp_bilinear_lds_kernel(WarpArgs a
                              : make_float4(q[0], x + 1 < a.W ? q[1] : 0.f, x + 2 < a.W ? q[2] : 0.f, 0.f);
     });
   };
-  load_box(0);
-  for (int c = 0; c < a.C; ++c) {
-    if (c) __syncthreads();  // every thread is done reading channel c-1's box
+  load_box(cb);
+  for (int c = cb; c < ce; ++c) {
+    if (c > cb) __syncthreads();  // every thread is done reading channel c-1's box
     chunk_walk([&](int j, int r, int col) { *reinterpret_cast<float4*>(&sBox[r * bw + col * 4]) = stage[j]; });
     __syncthreads();
-    if (c + 1 < a.C) load_box(c + 1);
+    if (c + 1 < ce) load_box(c + 1);
 #pragma unroll
     for (int k = 0; k < kWRows; ++k) {
       if (!((vmask >> (16 + k)) & 1u)) continue;
@@ -391,6 +398,8 @@ __global__ __launch_bounds__(kWThreads) void warp_bilinear_lds_kernel(WarpArgs a
 using namespace oflow;
 
 namespace {
+int g_warp_cpw = 0;  // channels per staged-tile workgroup (0: all; experiment hook oflow_exp_set_warp_cpw)
+
 template <bool FLOW>
 int launch_warp(const WarpArgs& a, int mode, hipStream_t s) {
   const long long total = (long long)a.B * a.Ho * a.Wo;
@@ -400,11 +409,12 @@ int launch_warp(const WarpArgs& a, int mode, hipStream_t s) {
     case OFLOW_INTERP_BILINEAR: {
       // LDS-staged tiles need 16-B frame rows for the box staging and H, W < 32768 for the packed tap coordinates
       const int tiles_x = (a.Wo + kWTX - 1) / kWTX, tiles_y = (a.Ho + kWTY - 1) / kWTY;
-      const long long nb = (long long)a.B * tiles_x * tiles_y;
+      const int cpw = g_warp_cpw > 0 ? std::min(g_warp_cpw, a.C) : a.C;
+      const long long nb = (long long)a.B * tiles_x * tiles_y * ((a.C + cpw - 1) / cpw);
       if ((a.W & 3) == 0 && (reinterpret_cast<uintptr_t>(a.frame) & 15) == 0 && a.W < 32768 && a.H < 32768 &&
           nb < (1ll << 31)) {
         hipLaunchKernelGGL((warp_bilinear_lds_kernel<FLOW>), dim3(static_cast<unsigned>(nb)), dim3(kWThreads), 0, s, a,
-                           tiles_x, tiles_y);
+                           tiles_x, tiles_y, cpw);
       } else {
         hipLaunchKernelGGL((grid_warp_kernel<OFLOW_INTERP_BILINEAR, FLOW>), grid, dim3(256), 0, s, a);
       }
@@ -444,3 +454,6 @@ extern "C" int oflow_grid_sample_f32(const float* d_input, const float* d_grid, 
   WarpArgs a{d_input, d_grid, d_out, B, C, H, W, Ho, Wo, padding_mode, align_corners ? 1 : 0};
   return launch_warp<false>(a, mode, static_cast<hipStream_t>(stream));
 }
+
+// experiment hook (not part of include/oflow.h): channels per LDS-staged warp workgroup (0 = all of the frame's)
+extern "C" void oflow_exp_set_warp_cpw(int cpw) { g_warp_cpw = cpw; }
