@@ -346,15 +346,24 @@ __global__ __launch_bounds__(64 * WM * WN, WM * WN == 8 ? 1 : 2) void conv_s32_k
     // the tile's input window (rows 2*ty0 - 3 .., columns 2*tx0 - 3 ..), zero padded (extractor.py:186 padding=3)
     const float* img = reinterpret_cast<const float*>(a.x) + (long long)b * kImgC * (2 * a.H) * (2 * a.W);
     const int iy0 = 2 * ty0 - kImgK / 2, ix0 = 2 * tx0 - kImgK / 2;
-    for (int e = tid; e < kImgC * kImgRows * kImgCols; e += NTH) {
+    // every load of the window issued before the first LDS store (clamped in-image addresses, zero selected after):
+    // a load -> store loop waited out one memory round trip per element (the stem ran 0.6 ms per 8 images)
+    constexpr int IMG_N = kImgC * kImgRows * kImgCols, IMG_PER = (IMG_N + NTH - 1) / NTH;
+    float iv[IMG_PER];
+#pragma unroll
+    for (int s_ = 0; s_ < IMG_PER; ++s_) {
+      const int e = min(tid + s_ * NTH, IMG_N - 1);
       const int ch = e / (kImgRows * kImgCols), rem = e - ch * (kImgRows * kImgCols);
       const int ry = rem / kImgCols, rx = rem - ry * kImgCols;
       const int iy = iy0 + ry, ix = ix0 + rx;
-      float v = 0.f;
-      if (static_cast<unsigned>(iy) < static_cast<unsigned>(2 * a.H) && static_cast<unsigned>(ix) < static_cast<unsigned>(2 * a.W))
-        v = img[((long long)ch * (2 * a.H) + iy) * (2 * a.W) + ix];
-      sImg[e] = v;
+      const bool in = static_cast<unsigned>(iy) < static_cast<unsigned>(2 * a.H) && static_cast<unsigned>(ix) < static_cast<unsigned>(2 * a.W);
+      const int cy = min(max(iy, 0), 2 * a.H - 1), cx = min(max(ix, 0), 2 * a.W - 1);
+      const float v = img[((long long)ch * (2 * a.H) + cy) * (2 * a.W) + cx];
+      iv[s_] = in ? v : 0.f;
     }
+#pragma unroll
+    for (int s_ = 0; s_ < IMG_PER; ++s_)
+      if (tid + s_ * NTH < IMG_N) sImg[tid + s_ * NTH] = iv[s_];
     // patch channel k = t*3 + ch, t = ky*7 + kx -> window offset ch*(rows*cols) + ky*cols + kx (-1: zero, k >= 147)
     for (int k = tid; k < 160; k += NTH) {
       const int t = k / kImgC, ch = k - t * kImgC;
@@ -499,15 +508,21 @@ __global__ __launch_bounds__(64 * WM * WN, WM * WN == 8 ? 1 : 2) void conv_s32_k
       // per-tile instance-norm partials of the conv output (merged by oflow_norm_stats_finalize): SL = 256 / BN
       // adjacent lanes share a channel and take interleaved slices of the tile's pixels (two-pass mean / M2 in
       // fp32); the slices are merged across those lanes with xor shuffles (Chan et al.).
+      // The partials' layout is 4-row x 32-column sub-tiles (oflow_conv_tiles): an 8-row tile writes its two 4-row
+      // halves as two partials, each computed exactly as a 4-row tile computes it (bit-identical statistics).
       constexpr int SL = NTH / BN >= 4 ? 4 : NTH / BN >= 2 ? 2 : 1;
       const int c = tid / SL, sl = tid % SL;
       const int n = n0 + c;
       const bool on = c < BN && n < a.N;
       const float ws = on ? sSB[c].x : 0.f, bi = on ? sSB[c].y : 0.f;
+      static_assert(TY % kTY == 0 || EPI != 0 || TY < kTY, "instance-norm partials: tiles of whole 4-row sub-tiles");
+      constexpr int SUB = kTY * kTX;  // pixels per 4-row partial
+      for (int sub = 0; sub < (BM >= SUB ? BM / SUB : 0); ++sub) {
+      const int pb = sub * SUB;
       int cnt = 0;
       float sum = 0.f;
       if (on) {
-        for (int pl = sl; pl < BM; pl += SL) {
+        for (int pl = pb + sl; pl < pb + SUB; pl += SL) {
           const int y = ty0 + pl / kTX, x = tx0 + (pl % kTX);
           if (y < a.H && x < a.W) {
             sum += sT[pl * TS + c] * ws + bi;
@@ -517,7 +532,7 @@ __global__ __launch_bounds__(64 * WM * WN, WM * WN == 8 ? 1 : 2) void conv_s32_k
       }
       float N0 = static_cast<float>(cnt), M0 = cnt ? sum / N0 : 0.f, Q0 = 0.f;
       if (on) {
-        for (int pl = sl; pl < BM; pl += SL) {
+        for (int pl = pb + sl; pl < pb + SUB; pl += SL) {
           const int y = ty0 + pl / kTX, x = tx0 + (pl % kTX);
           if (y < a.H && x < a.W) {
             const float d = sT[pl * TS + c] * ws + bi - M0;
@@ -545,12 +560,14 @@ __global__ __launch_bounds__(64 * WM * WN, WM * WN == 8 ? 1 : 2) void conv_s32_k
           N0 = nn;
         }
       }
-      if (on && sl == 0) {
-        const int tile_in_img = (ty0 / TY) * a.tiles_x + tx0 / kTX;
-        float* st = a.stats + (((long long)b * a.tiles_x * a.tiles_y + tile_in_img) * a.npad + n) * 3;
+      if (on && sl == 0 && ty0 + sub * kTY < a.H) {
+        const int tiles4_y = (a.H + kTY - 1) / kTY;
+        const int tile_in_img = (ty0 / kTY + sub) * a.tiles_x + tx0 / kTX;
+        float* st = a.stats + (((long long)b * a.tiles_x * tiles4_y + tile_in_img) * a.npad + n) * 3;
         st[0] = N0;
         st[1] = M0;
         st[2] = Q0;
+      }
       }
     }
     if (a.y0 == nullptr && a.fn == nullptr) return;
@@ -707,6 +724,9 @@ int launch_conv(const ConvArgs& a0, hipStream_t s) {
 // In-process A/B (tools/exp/run_small_grid_ab.py): batch 1 x 24 iterations 12.9 -> 8.8 ms; a pixel threshold keeps
 // the 4-pair lanes of the 8-pair step (28160 px) on the default tiles, where the small ones cost +1.5-3 %.
 int g_small_grid_px = 16384;  // output-pixel count under which the small tiles are used (0: never; experiments only)
+// instance-norm convs (encoders, BN 64) on 8-row tiles too (0: 4-row tiles; experiments only). Step A/B, back-to-back
+// processes on one box: 8-row 21.07-21.12 ms vs 4-row 21.29-21.33 (profiles/r03/s7_*); outputs bit-identical.
+int g_stats_8row = 1;
 inline bool small_grid(const ConvArgs& a, int bn) {
   return (long long)a.B * a.H * a.W < g_small_grid_px && a.stats == nullptr && a.ain == kInS32 && a.npad % 64 == 0 &&
          bn >= 64;
@@ -719,11 +739,11 @@ int launch_bn(const ConvArgs& a, int bn, hipStream_t s) {
     case 128: return launch_conv<KH, KW, 128, 2, 2, EPI>(a, s);
     case 96: return launch_conv<KH, KW, 96, 4, 1, EPI>(a, s);
     case 64:
-      // 8-row tiles (each wave 64 px x 64 ch: 8 operand reads per 12 MFMAs instead of 6 per 6), except with
-      // instance-norm partials, whose layout is 4-row tiles
+      // 8-row tiles (each wave 64 px x 64 ch: 8 operand reads per 12 MFMAs instead of 6 per 6); instance-norm
+      // partials are written per 4-row half
       // (1x1 convs double-buffer the 8-row halo: 4-row tiles keep two workgroups per CU within the LDS)
       if constexpr (KH * KW > 1)
-        if (a.stats == nullptr) return launch_conv<KH, KW, 64, 4, 1, EPI, 8>(a, s);
+        if (a.stats == nullptr || g_stats_8row) return launch_conv<KH, KW, 64, 4, 1, EPI, 8>(a, s);
       return launch_conv<KH, KW, 64, 2, 2, EPI>(a, s);
     case 32: return launch_conv<KH, KW, 32, 4, 1, EPI>(a, s);
     default: return OFLOW_E_SHAPE;
@@ -930,3 +950,4 @@ extern "C" int oflow_conv_s32(const void* d_x, long long x_pixel_stride, int in_
 
 // experiment hook (not part of include/oflow.h): the small-grid pixel threshold, for in-process A/B runs (tools/exp)
 extern "C" void oflow_exp_set_small_grid_px(int pixels) { oflow::g_small_grid_px = pixels; }
+extern "C" void oflow_exp_set_stats_8row(int on) { oflow::g_stats_8row = on; }
