@@ -1,6 +1,7 @@
 """In-process A/B of RAFT model attributes on the Sintel x8 step (12 iterations, test mode): ATTRS (JSON) maps an arm
 name to {attribute: value}; the arms run interleaved (3 forwards per sample, SAMPLES samples each), and the flows of
-every arm are compared with the first arm's (bit-identical or max |d|). Prints one JSON line.
+every arm are compared with the first arm's (bit-identical or max |d|). An attribute "lib:<symbol>" calls that
+experiment hook of the native library with the value instead. Prints one JSON line.
   ATTRS='{"patch": {"stem_from_image": false}, "image": {"stem_from_image": true}}' python tools/exp/attr_ab.py"""
 import json
 import os
@@ -30,9 +31,14 @@ def main():
     res = {k: [] for k in arms}
     outs = {}
 
+    from optical_flow import _native as N
+
     def setarm(k):
         for attr, v in arms[k].items():
-            setattr(model, attr, v)
+            if attr.startswith("lib:"):  # an experiment hook of the native library: lib:<symbol> = int argument
+                getattr(N.load(), attr[4:])(int(v))
+            else:
+                setattr(model, attr, v)
 
     with torch.inference_mode():
         for k in arms:

@@ -79,6 +79,7 @@ struct ConvArgs {
   int ain;                 // input format: kInS32 / kInF32Norm / kInF32
   int cin;                 // kInF32: real input channels (row pitch cin * 4 B); channels >= cin stage as zeros
   int wbytes;              // bytes of the packed weights (kg * taps * npad * 128)
+  int exp_flags;           // experiments only (oflow_exp_set_conv_flags): bit 0 = the stem's element-wise window loop
 };
 // input formats of oflow_conv_s32_ex2
 constexpr int kInS32 = OFLOW_IN_S32, kInF32Norm = OFLOW_IN_F32_NORM, kInF32 = OFLOW_IN_F32, kInImg = OFLOW_IN_IMG7S2;
@@ -349,6 +350,17 @@ __global__ __launch_bounds__(64 * WM * WN, WM * WN == 8 ? 1 : 2) void conv_s32_k
     // every load of the window issued before the first LDS store (clamped in-image addresses, zero selected after):
     // a load -> store loop waited out one memory round trip per element (the stem ran 0.6 ms per 8 images)
     constexpr int IMG_N = kImgC * kImgRows * kImgCols, IMG_PER = (IMG_N + NTH - 1) / NTH;
+    if (a.exp_flags & 1) {  // experiment: the element-wise load -> store loop
+      for (int e = tid; e < IMG_N; e += NTH) {
+        const int ch = e / (kImgRows * kImgCols), rem = e - ch * (kImgRows * kImgCols);
+        const int ry = rem / kImgCols, rx = rem - ry * kImgCols;
+        const int iy = iy0 + ry, ix = ix0 + rx;
+        float v = 0.f;
+        if (static_cast<unsigned>(iy) < static_cast<unsigned>(2 * a.H) && static_cast<unsigned>(ix) < static_cast<unsigned>(2 * a.W))
+          v = img[((long long)ch * (2 * a.H) + iy) * (2 * a.W) + ix];
+        sImg[e] = v;
+      }
+    } else {
     float iv[IMG_PER];
 #pragma unroll
     for (int s_ = 0; s_ < IMG_PER; ++s_) {
@@ -364,6 +376,7 @@ __global__ __launch_bounds__(64 * WM * WN, WM * WN == 8 ? 1 : 2) void conv_s32_k
 #pragma unroll
     for (int s_ = 0; s_ < IMG_PER; ++s_)
       if (tid + s_ * NTH < IMG_N) sImg[tid + s_ * NTH] = iv[s_];
+    }
     // patch channel k = t*3 + ch, t = ky*7 + kx -> window offset ch*(rows*cols) + ky*cols + kx (-1: zero, k >= 147)
     for (int k = tid; k < 160; k += NTH) {
       const int t = k / kImgC, ch = k - t * kImgC;
@@ -724,9 +737,12 @@ int launch_conv(const ConvArgs& a0, hipStream_t s) {
 // In-process A/B (tools/exp/run_small_grid_ab.py): batch 1 x 24 iterations 12.9 -> 8.8 ms; a pixel threshold keeps
 // the 4-pair lanes of the 8-pair step (28160 px) on the default tiles, where the small ones cost +1.5-3 %.
 int g_small_grid_px = 16384;  // output-pixel count under which the small tiles are used (0: never; experiments only)
-// instance-norm convs (encoders, BN 64) on 8-row tiles too (0: 4-row tiles; experiments only). Step A/B, back-to-back
-// processes on one box: 8-row 21.07-21.12 ms vs 4-row 21.29-21.33 (profiles/r03/s7_*); outputs bit-identical.
-int g_stats_8row = 1;
+// instance-norm convs (encoders, BN 64) on 8-row tiles too (experiments only; outputs bit-identical). Alone the 8-row
+// tiles are 0-12 % faster per layer, but in the step, where fnet's halves and cnet share the chip, their 71 KB of LDS
+// per workgroup crowds the other streams' workgroups: interleaved in-process A/B 20.40 (4-row) vs 20.69-20.90 ms
+// (profiles/r03/exp/s8b_ab_enc.log).
+int g_stats_8row = 0;
+int g_conv_exp_flags = 0;
 inline bool small_grid(const ConvArgs& a, int bn) {
   return (long long)a.B * a.H * a.W < g_small_grid_px && a.stats == nullptr && a.ain == kInS32 && a.npad % 64 == 0 &&
          bn >= 64;
@@ -846,6 +862,7 @@ int build_conv_args(ConvArgs& a, const void* d_x, long long x_pixel_stride, int 
   const long long wbytes = (long long)in_groups * kh * kw * n_pad * 128;
   if (wbytes >= (1ll << 31) || (long long)H * W * x_pixel_stride >= (1ll << 31)) return OFLOW_E_SHAPE;
   a.wbytes = static_cast<int>(wbytes);
+  a.exp_flags = g_conv_exp_flags;
   (void)block_n;
   return OFLOW_OK;
 }
@@ -951,3 +968,4 @@ extern "C" int oflow_conv_s32(const void* d_x, long long x_pixel_stride, int in_
 // experiment hook (not part of include/oflow.h): the small-grid pixel threshold, for in-process A/B runs (tools/exp)
 extern "C" void oflow_exp_set_small_grid_px(int pixels) { oflow::g_small_grid_px = pixels; }
 extern "C" void oflow_exp_set_stats_8row(int on) { oflow::g_stats_8row = on; }
+extern "C" void oflow_exp_set_conv_flags(int flags) { oflow::g_conv_exp_flags = flags; }

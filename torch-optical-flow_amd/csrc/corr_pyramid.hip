@@ -243,7 +243,7 @@ __device__ __forceinline__ void pyramid_epilogue(const PyramidArgs& p, f32x16 (&
         const float a0 = v1[0][r], c0 = v1[1][r];
         v2[pr][r] = pool4(a0, dpp_xor2(a0), c0, dpp_xor2(c0));
         const int i = qbase + (r & 3) + 8 * (r >> 2);
-        if (ok && i < p.N) p.lv[2][lvl_off<TILED>(p, 2, (size_t)b * Nn + i, y2, x2)] = v2[pr][r];
+        if (!TILED && ok && i < p.N) p.lv[2][lvl_off<TILED>(p, 2, (size_t)b * Nn + i, y2, x2)] = v2[pr][r];
       }
     }
   }
@@ -261,6 +261,51 @@ __device__ __forceinline__ void pyramid_epilogue(const PyramidArgs& p, f32x16 (&
       if (i < p.N && (y1 >> 2) < p.HB[1] && (ch >> 3) < tb1)
         *reinterpret_cast<float4*>(&p.lv[1][lvl_off<true>(p, 1, (size_t)b * Nn + i, y1, tx0 >> 1) + ch * 4]) = v;
     }
+    if (p.nlev < 3) return;
+    // levels 2 and 3 through LDS as well: per query, level 2 of this tile is 2 rows x 8 columns = 64 contiguous bytes
+    // of one 4x8 tile (ty0 / 4 is even, tx0 / 4 a multiple of 8) and level 3 one row x 4 columns = 16 contiguous bytes,
+    // so a wave writes 16-B chunks (3 store instructions) instead of 48 scalar stores of 8 or 16 lanes
+    float v3[16];
+    if (p.nlev >= 4) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const float a0 = v2[0][r], c0 = v2[1][r];
+        v3[r] = pool4(a0, swz_xor4(a0), c0, swz_xor4(c0));
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();  // level 1's LDS reads are done before the scratch is reused
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    float* s2 = sbuf + wave * 2048;  // level 2: [query 32][row 2][col 8]; level 3 at +512: [query 32][col 4]
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int ql = (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+      if ((tx & 3) == 0) {
+        s2[ql * 16 + (tx >> 2)] = v2[0][r];
+        s2[ql * 16 + 8 + (tx >> 2)] = v2[1][r];
+      }
+      if (p.nlev >= 4 && (tx & 7) == 0) s2[512 + ql * 4 + (tx >> 3)] = v3[r];
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    const int y2 = ty0 >> 2, x2 = tx0 >> 2;
+#pragma unroll
+    for (int it = 0; it < 2; ++it) {
+      const int c = lane + 64 * it, ql = c >> 2, part = c & 3;
+      const int i = i0 + wave * 32 + ql;
+      const float4 v = *reinterpret_cast<const float4*>(&s2[ql * 16 + part * 4]);
+      if (i < p.N && (y2 >> 2) < p.HB[2] && (x2 >> 3) < p.WB[2])
+        *reinterpret_cast<float4*>(&p.lv[2][lvl_off<true>(p, 2, (size_t)b * Nn + i, y2, x2) + part * 4]) = v;
+    }
+    if (p.nlev >= 4 && lane < 32) {
+      const int y3 = ty0 >> 3, x3 = tx0 >> 3;
+      const int i = i0 + wave * 32 + lane;
+      const float4 v = *reinterpret_cast<const float4*>(&s2[512 + lane * 4]);
+      if (i < p.N && (y3 >> 2) < p.HB[3] && (x3 >> 3) < p.WB[3])
+        *reinterpret_cast<float4*>(&p.lv[3][lvl_off<true>(p, 3, (size_t)b * Nn + i, y3, x3)]) = v;
+    }
+    return;
   }
   if (p.nlev < 4) return;
   {
