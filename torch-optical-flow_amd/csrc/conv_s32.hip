@@ -743,6 +743,10 @@ int g_small_grid_px = 16384;  // output-pixel count under which the small tiles 
 // (profiles/r03/exp/s8b_ab_enc.log).
 int g_stats_8row = 0;
 int g_conv_exp_flags = 0;
+// BN 64 convs without instance-norm partials (cnet's layer1, convc2, the motion conv) on 8-row tiles (experiments
+// only). r02 adopted them from per-layer timings; in the step (concurrent streams) the 4-row tiles win: interleaved
+// in-process A/B 20.36 vs 20.53-20.55 ms (profiles/r03/exp/s9_ab_bn64.log).
+int g_bn64_8row = 0;
 inline bool small_grid(const ConvArgs& a, int bn) {
   return (long long)a.B * a.H * a.W < g_small_grid_px && a.stats == nullptr && a.ain == kInS32 && a.npad % 64 == 0 &&
          bn >= 64;
@@ -759,7 +763,7 @@ int launch_bn(const ConvArgs& a, int bn, hipStream_t s) {
       // partials are written per 4-row half
       // (1x1 convs double-buffer the 8-row halo: 4-row tiles keep two workgroups per CU within the LDS)
       if constexpr (KH * KW > 1)
-        if (a.stats == nullptr || g_stats_8row) return launch_conv<KH, KW, 64, 4, 1, EPI, 8>(a, s);
+        if (a.stats == nullptr ? g_bn64_8row != 0 : g_stats_8row != 0) return launch_conv<KH, KW, 64, 4, 1, EPI, 8>(a, s);
       return launch_conv<KH, KW, 64, 2, 2, EPI>(a, s);
     case 32: return launch_conv<KH, KW, 32, 4, 1, EPI>(a, s);
     default: return OFLOW_E_SHAPE;
@@ -969,3 +973,4 @@ extern "C" int oflow_conv_s32(const void* d_x, long long x_pixel_stride, int in_
 extern "C" void oflow_exp_set_small_grid_px(int pixels) { oflow::g_small_grid_px = pixels; }
 extern "C" void oflow_exp_set_stats_8row(int on) { oflow::g_stats_8row = on; }
 extern "C" void oflow_exp_set_conv_flags(int flags) { oflow::g_conv_exp_flags = flags; }
+extern "C" void oflow_exp_set_bn64_8row(int on) { oflow::g_bn64_8row = on; }
