@@ -372,3 +372,41 @@ def test_flow_head2_arg_errors():
         N.flow_head2(N.S32Slice(xs), wt, None, coords)  # bias required
     with pytest.raises(RuntimeError):
         N.flow_head2(N.S32Slice(xs), wt, bias, coords[:, :, :4])
+
+
+@pytest.mark.parametrize("kh,c,n,bn,h,w,tiles8", [(3, 64, 64, 64, 37, 70, 0), (3, 64, 64, 64, 37, 70, 1),
+                                                   (3, 96, 96, 96, 21, 40, 0), (3, 128, 128, 128, 13, 33, 0),
+                                                   (1, 64, 96, 96, 16, 64, 0), (2, 256, 128, 128, 11, 20, 0)])
+def test_instance_norm_partials(kh, c, n, bn, h, w, tiles8):
+    """The conv epilogue's per-tile instance-norm partials (count, mean, M2 from the accumulators: per lane, lane
+    halves, then the waves of each 4-row sub-tile) merged by oflow_norm_stats_finalize = the per-(image, channel)
+    mean / variance of the conv's own fp32 output computed in float64 (extractor.py:75-76, nn.InstanceNorm2d eps 1e-5):
+    alpha = 1/sqrt(var + eps) and beta = -mean * alpha to 2e-6 relative (fp32 partial sums over <= 128 pixels); ragged
+    H and W (partial tiles), 4-row and 8-row tiles (oflow_exp_set_stats_8row), 64 / 96 / 128-channel blocks."""
+    import ctypes
+    b = 2
+    g = torch.Generator().manual_seed(11 + kh + n + tiles8)
+    x = (torch.randn(b, c, h, w, generator=g) * 2 + 0.3).to(DEV)
+    wt = (torch.randn(n, c, kh, kh, generator=g) * 0.05).to(DEV)
+    cw = N.ConvWeights(wt, torch.randn(n, generator=g).to(DEV) * 0.5, ((n + 31) // 32) * 32)
+    tiles = N.conv_tiles(h, w)
+    raw = torch.empty(b * h * w, n, device=DEV)
+    part = torch.full((b, tiles, cw.n_pad, 3), float("nan"), device=DEV)
+    lib = N.load()
+    lib.oflow_exp_set_stats_8row.argtypes = [ctypes.c_int]
+    lib.oflow_exp_set_stats_8row(tiles8)
+    try:
+        N.conv_s32(N.S32Slice(N.s32_from_f32(x)), cw, bn, nhwc=raw, stats=part)
+        alpha, beta = N.norm_stats(part, b, tiles, cw.n_pad, n, 1e-5)
+        torch.cuda.synchronize()
+    finally:
+        lib.oflow_exp_set_stats_8row(0)
+    y = raw.view(b, h * w, n).double()
+    mean = y.mean(dim=1)
+    var = y.var(dim=1, unbiased=False)
+    a_ref = 1.0 / torch.sqrt(var + 1e-5)
+    b_ref = -mean * a_ref
+    assert torch.isfinite(part[..., :n, :]).all()
+    ea = float(((alpha.double() - a_ref).abs() / a_ref).max())
+    eb = float(((beta.double() - b_ref).abs() / (mean.abs() * a_ref + 1.0)).max())
+    assert ea <= 2e-6 and eb <= 2e-6, (ea, eb)

@@ -1,7 +1,7 @@
 """In-process A/B of RAFT model attributes on the Sintel x8 step (12 iterations, test mode): ATTRS (JSON) maps an arm
 name to {attribute: value}; the arms run interleaved (3 forwards per sample, SAMPLES samples each), and the flows of
 every arm are compared with the first arm's (bit-identical or max |d|). An attribute "lib:<symbol>" calls that
-experiment hook of the native library with the value instead. Prints one JSON line.
+experiment hook of the native library with the value instead, "bn:<layer>" sets model.update.CONV_BN[layer]. Prints one JSON line.
   ATTRS='{"patch": {"stem_from_image": false}, "image": {"stem_from_image": true}}' python tools/exp/attr_ab.py"""
 import json
 import os
@@ -37,6 +37,9 @@ def main():
         for attr, v in arms[k].items():
             if attr.startswith("lib:"):  # an experiment hook of the native library: lib:<symbol> = int argument
                 getattr(N.load(), attr[4:])(int(v))
+            elif attr.startswith("bn:"):  # an update-block conv's output-channel block (model.update.CONV_BN)
+                from model import update as U
+                U.CONV_BN[attr[3:]] = int(v)
             else:
                 setattr(model, attr, v)
 

@@ -34,6 +34,14 @@ typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));  // native vecto
 __device__ __forceinline__ int swz(int row) { return (row >> 1) & 7; }
 
 constexpr int kTY = 4, kTX = 32;  // default tile: kTY rows x kTX columns
+
+// ablation build (tools/exp: -DOFLOW_ABLATE): exp_flags bits drop parts of the kernel to time the rest; the product
+// build compiles every test to false
+#ifdef OFLOW_ABLATE
+#define OFLOW_ABL(bit) ((a.exp_flags & (bit)) != 0)
+#else
+#define OFLOW_ABL(bit) false
+#endif
 constexpr int kAinGroups = 4;                      // AIN inputs: up to 128 channels (the encoders' 64 / 96 / 128)
 
 
@@ -172,6 +180,8 @@ __global__ __launch_bounds__(64 * WM * WN, WM * WN == 8 ? 1 : 2) void conv_s32_k
   // the block's per-channel (inverse weight scale, bias), staged once for the epilogue (whose loops would otherwise
   // wait on a global-load round trip per iteration)
   __shared__ float2 sSB[BN];
+  // instance-norm partials per (row of waves, channel): (count, mean, M2)
+  __shared__ float3 sStat[EPI == 0 ? WM * BN : 1];
   float2* sAff = reinterpret_cast<float2*>(smem + LDS_BYTES);
   float* sImg = reinterpret_cast<float*>(smem + LDS_BYTES);  // kInImg: [c][row][col], zero at kImgZero
   int* sKoff = reinterpret_cast<int*>(smem + LDS_BYTES + (AIN == kInImg ? IMG_FLOATS * 4 : 0));
@@ -237,7 +247,7 @@ __global__ __launch_bounds__(64 * WM * WN, WM * WN == 8 ? 1 : 2) void conv_s32_k
       RA[s_] = __builtin_amdgcn_raw_buffer_load_b128(rsA, off_, (G) * 128, 0);                                      \
   }
 #define OFLOW_WRITE_A(RA, BUF, G)                                                                                    \
-  _Pragma("unroll") for (int s_ = 0; s_ < APER; ++s_) {                                                              \
+  if (!OFLOW_ABL(4)) _Pragma("unroll") for (int s_ = 0; s_ < APER; ++s_) {                                           \
     const int item = tid + s_ * NTH;                                                                            \
     const int p = item >> 3, c = item & 7;                                                                           \
     if (AITEMS % NTH == 0 || item < AITEMS) {                                                                   \
@@ -318,7 +328,7 @@ __global__ __launch_bounds__(64 * WM * WN, WM * WN == 8 ? 1 : 2) void conv_s32_k
   }
   // hi*lo + lo*hi + hi*hi per (pixel tile, channel tile): the lo*lo term is below fp32 rounding
 #define OFLOW_MFMAS(AH, AL, BH, BL)                                                                                  \
-  _Pragma("unroll") for (int mt = 0; mt < MT; ++mt)                                                                  \
+  if (!OFLOW_ABL(2)) _Pragma("unroll") for (int mt = 0; mt < MT; ++mt)                                               \
     _Pragma("unroll") for (int nt = 0; nt < NT; ++nt) {                                                              \
       acc[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(AH[mt], BL[nt], acc[mt][nt], 0, 0, 0);                    \
       acc[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(AL[mt], BH[nt], acc[mt][nt], 0, 0, 0);                    \
@@ -478,6 +488,59 @@ __global__ __launch_bounds__(64 * WM * WN, WM * WN == 8 ? 1 : 2) void conv_s32_k
         sT[(pbase + m) * TS + nl] = acc[mt][nt][e];
       }
     }
+  if constexpr (EPI == 0 && TY >= kTY) {
+    if (a.stats != nullptr && !OFLOW_ABL(8)) {
+      // instance-norm partials of the conv output (merged by oflow_norm_stats_finalize), from the accumulators: each
+      // lane holds one channel of this wave's MT rows (16 pixels per row and lane half); two-pass mean / M2 over its
+      // values in fp32, merged with the other lane half (xor 32) and then, per 4-row sub-tile, across the waves that
+      // cover it (sStat, after the barrier)
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt) {
+        const int nl = wn * (BN / WN) + nt * 32 + r;
+        const float2 sb = sSB[nl];
+        float cnt = 0.f, sum = 0.f;
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt) {
+          const bool yok = ty0 + wm * MT + mt < a.H;
+#pragma unroll
+          for (int e = 0; e < 16; ++e) {
+            const bool ok = yok && tx0 + (e & 3) + 8 * (e >> 2) + 4 * hh < a.W;
+            sum += ok ? acc[mt][nt][e] * sb.x + sb.y : 0.f;
+            cnt += ok ? 1.f : 0.f;
+          }
+        }
+        const float mean = cnt > 0.f ? sum / cnt : 0.f;
+        float q = 0.f;
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt) {
+          const bool yok = ty0 + wm * MT + mt < a.H;
+#pragma unroll
+          for (int e = 0; e < 16; ++e) {
+            const bool ok = yok && tx0 + (e & 3) + 8 * (e >> 2) + 4 * hh < a.W;
+            const float d = (acc[mt][nt][e] * sb.x + sb.y) - mean;
+            q += ok ? d * d : 0.f;
+          }
+        }
+        // merge with lane ^ 32 (symmetric: both lanes compute the same value; lane half 0 first)
+        const float nb = __shfl_xor(cnt, 32), mb = __shfl_xor(mean, 32), qb = __shfl_xor(q, 32);
+        const float n0_ = hh ? nb : cnt, m0_ = hh ? mb : mean, q0_ = hh ? qb : q;
+        const float n1_ = hh ? cnt : nb, m1_ = hh ? mean : mb, q1_ = hh ? q : qb;
+        const float nn = n0_ + n1_;
+        float M = m0_, Q = q0_;
+        if (n1_ > 0.f) {
+          if (n0_ > 0.f) {
+            const float d = m1_ - m0_;
+            M = m0_ + d * (n1_ / nn);
+            Q = q0_ + q1_ + d * d * (n0_ * n1_ / nn);
+          } else {
+            M = m1_;
+            Q = q1_;
+          }
+        }
+        if (hh == 0) sStat[wm * BN + nl] = make_float3(nn, M, Q);
+      }
+    }
+  }
   __syncthreads();
   if (has_add) {
     // pre-activation value = acc * scale + bias + addend, in place (each thread rewrites only its own items, which it
@@ -517,73 +580,41 @@ __global__ __launch_bounds__(64 * WM * WN, WM * WN == 8 ? 1 : 2) void conv_s32_k
     }
   }
   if constexpr (EPI == 0) {
-    if (a.stats != nullptr) {
-      // per-tile instance-norm partials of the conv output (merged by oflow_norm_stats_finalize): SL = 256 / BN
-      // adjacent lanes share a channel and take interleaved slices of the tile's pixels (two-pass mean / M2 in
-      // fp32); the slices are merged across those lanes with xor shuffles (Chan et al.).
-      // The partials' layout is 4-row x 32-column sub-tiles (oflow_conv_tiles): an 8-row tile writes its two 4-row
-      // halves as two partials, each computed exactly as a 4-row tile computes it (bit-identical statistics).
-      constexpr int SL = NTH / BN >= 4 ? 4 : NTH / BN >= 2 ? 2 : 1;
-      const int c = tid / SL, sl = tid % SL;
-      const int n = n0 + c;
-      const bool on = c < BN && n < a.N;
-      const float ws = on ? sSB[c].x : 0.f, bi = on ? sSB[c].y : 0.f;
-      static_assert(TY % kTY == 0 || EPI != 0 || TY < kTY, "instance-norm partials: tiles of whole 4-row sub-tiles");
-      constexpr int SUB = kTY * kTX;  // pixels per 4-row partial
-      for (int sub = 0; sub < (BM >= SUB ? BM / SUB : 0); ++sub) {
-      const int pb = sub * SUB;
-      int cnt = 0;
-      float sum = 0.f;
-      if (on) {
-        for (int pl = pb + sl; pl < pb + SUB; pl += SL) {
-          const int y = ty0 + pl / kTX, x = tx0 + (pl % kTX);
-          if (y < a.H && x < a.W) {
-            sum += sT[pl * TS + c] * ws + bi;
-            ++cnt;
-          }
-        }
-      }
-      float N0 = static_cast<float>(cnt), M0 = cnt ? sum / N0 : 0.f, Q0 = 0.f;
-      if (on) {
-        for (int pl = pb + sl; pl < pb + SUB; pl += SL) {
-          const int y = ty0 + pl / kTX, x = tx0 + (pl % kTX);
-          if (y < a.H && x < a.W) {
-            const float d = sT[pl * TS + c] * ws + bi - M0;
-            Q0 += d * d;
-          }
-        }
-      }
+    if (a.stats != nullptr && !OFLOW_ABL(8)) {
+      // per-4-row-sub-tile partials from the waves' (count, mean, M2) in sStat, merged in wave order (Chan et al.)
+      if constexpr (TY >= kTY) {
+        constexpr int NSUB = TY / kTY, WPS = kTY / MT;  // sub-tiles per tile, waves (rows of waves) per sub-tile
+        if (tid < BN * NSUB) {
+          const int c = tid % BN, sub = tid / BN, n = n0 + c;
+          float N0 = 0.f, M0 = 0.f, Q0 = 0.f;
 #pragma unroll
-      for (int m = 1; m < SL; m <<= 1) {
-        const float nb = __shfl_xor(N0, m), mb = __shfl_xor(M0, m), qb = __shfl_xor(Q0, m);
-        const float nn = N0 + nb;
-        if (nb > 0.f) {
-          // symmetric form: both lanes of a pair compute the identical merged value
-          const float lo_n = (sl & m) ? nb : N0, hi_n = (sl & m) ? N0 : nb;
-          const float lo_m = (sl & m) ? mb : M0, hi_m = (sl & m) ? M0 : mb;
-          const float lo_q = (sl & m) ? qb : Q0, hi_q = (sl & m) ? Q0 : qb;
-          if (lo_n > 0.f) {
-            const float d = hi_m - lo_m;
-            M0 = lo_m + d * (hi_n / nn);
-            Q0 = lo_q + hi_q + d * d * (lo_n * hi_n / nn);
-          } else {
-            M0 = hi_m;
-            Q0 = hi_q;
+          for (int j = 0; j < WPS; ++j) {
+            const float3 t = sStat[(sub * WPS + j) * BN + c];
+            const float nn = N0 + t.x;
+            if (t.x > 0.f) {
+              if (N0 > 0.f) {
+                const float d = t.y - M0;
+                M0 = M0 + d * (t.x / nn);
+                Q0 = Q0 + t.z + d * d * (N0 * t.x / nn);
+              } else {
+                M0 = t.y;
+                Q0 = t.z;
+              }
+              N0 = nn;
+            }
           }
-          N0 = nn;
+          if (n < a.N && ty0 + sub * kTY < a.H) {
+            const int tiles4_y = (a.H + kTY - 1) / kTY;
+            const int tile_in_img = (ty0 / kTY + sub) * a.tiles_x + tx0 / kTX;
+            float* st = a.stats + (((long long)b * a.tiles_x * tiles4_y + tile_in_img) * a.npad + n) * 3;
+            st[0] = N0;
+            st[1] = M0;
+            st[2] = Q0;
+          }
         }
-      }
-      if (on && sl == 0 && ty0 + sub * kTY < a.H) {
-        const int tiles4_y = (a.H + kTY - 1) / kTY;
-        const int tile_in_img = (ty0 / kTY + sub) * a.tiles_x + tx0 / kTX;
-        float* st = a.stats + (((long long)b * a.tiles_x * tiles4_y + tile_in_img) * a.npad + n) * 3;
-        st[0] = N0;
-        st[1] = M0;
-        st[2] = Q0;
-      }
       }
     }
-    if (a.y0 == nullptr && a.fn == nullptr) return;
+    if ((a.y0 == nullptr && a.fn == nullptr) || OFLOW_ABL(16)) return;
   }
 
   // S32 / GRU consumers: one thread = one pixel x 8 consecutive channels, KIT items per thread. The GRU state operands
