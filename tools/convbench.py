@@ -48,8 +48,14 @@ def main():
     ap.add_argument("--iters", type=int, default=30)
     ap.add_argument("--layer", default=None, help="only layers whose name contains this string (PMC runs)")
     ap.add_argument("--no-lookup", action="store_true")
+    ap.add_argument("--ablate", action="store_true", help="with the -DOFLOW_ABLATE library build (OFLOW_LIB): per-layer "
+                    "times with kernel parts dropped (exp_flags: 2 MFMAs, 4 A staging, 16 epilogue, 32 B staging, "
+                    "64 main-loop barriers)")
+    ap.add_argument("--shape-batch", type=int, default=0, help="override the batch (pairs) of --shape")
     args = ap.parse_args()
     b, h, w = SHAPES[args.shape]
+    if args.shape_batch:
+        b = args.shape_batch
     dev = torch.device("cuda", 0)
     P = b * h * w
     g = torch.Generator().manual_seed(0)
@@ -71,10 +77,11 @@ def main():
         ("convf1 1x1 128->128", 1, 1, 128, 128, 128, 128, 4, 4, 0),
         ("convf2 3x3 128->64", 3, 3, 128, 64, 64, 64, 4, 2, 0),
         ("conv 3x3 256->126", 3, 3, 256, 126, 128, 128, 8, 4, 0),
-        ("gru zr 1x5 384->256", 1, 5, 384, 256, 256, 128, 12, 4, 1),
-        ("gru q 1x5 384->128", 1, 5, 384, 128, 128, 128, 12, 4, 2),
-        ("gru zr 5x1 384->256", 5, 1, 384, 256, 256, 128, 12, 4, 1),
-        ("gru q 5x1 384->128", 5, 1, 384, 128, 128, 128, 12, 4, 2),
+        # the GRU convs contract [h | motion | flow] (8 groups); the context term W_inp*inp + b comes as the addend
+        ("gru zr 1x5 256->256", 1, 5, 256, 256, 256, 128, 8, 4, 1),
+        ("gru q 1x5 256->128", 1, 5, 256, 128, 128, 128, 8, 4, 2),
+        ("gru zr 5x1 256->256", 5, 1, 256, 256, 256, 128, 8, 4, 1),
+        ("gru q 5x1 256->128", 5, 1, 256, 128, 128, 128, 8, 4, 2),
         ("fh1 3x3 128->256", 3, 3, 128, 256, 256, 128, 4, 8, 0),
         ("fh2 3x3 256->2", 3, 3, 256, 2, 32, 32, 8, 0, 0),
     ]
@@ -87,13 +94,21 @@ def main():
         cw = weights(n, cin, kh, kw, npad)
         kw_ = {}
         if epi:
-            kw_ = dict(epilogue=epi, y0=N.S32Slice(N.s32_empty(b, h, w, 4, dev)), gru_h=hm, gru_z=z)
+            kw_ = dict(epilogue=epi, y0=N.S32Slice(N.s32_empty(b, h, w, 4, dev)), gru_h=hm, gru_z=z,
+                       addend=torch.randn(P, n, device=dev))
         elif go:
             kw_ = dict(act="relu", y0=N.S32Slice(N.s32_empty(b, h, w, go, dev)))
         else:
             kw_ = dict(f32=torch.zeros(b, 2, h, w, device=dev), f32_accumulate=True)
         ms = timed(lambda: N.conv_s32(N.S32Slice(x), cw, bn, **kw_), args.iters)
         total += ms
+        if args.ablate:  # the -DOFLOW_ABLATE library: time with parts of the kernel dropped
+            lib = N.load()
+            abl = {}
+            for f in (2, 4, 16, 32, 64, 2 | 4 | 32, 2 | 4 | 16 | 32 | 64):
+                lib.oflow_exp_set_conv_flags(f)
+                abl[str(f)] = round(timed(lambda: N.conv_s32(N.S32Slice(x), cw, bn, **kw_), args.iters) * 1e3, 1)
+            lib.oflow_exp_set_conv_flags(0)
         flops = 2.0 * P * n * cin * kh * kw
         padded = 2.0 * P * npad * (gi * 32) * kh * kw * 3
         out["layers"][name] = {
@@ -101,6 +116,8 @@ def main():
             "tflops_f32_equiv": round(flops / ms / 1e9, 1),
             "mfma_frac": round(padded / (ms * 1e-3) / F16_PEAK, 3),
         }
+        if args.ablate:
+            out["layers"][name]["ablated_us"] = abl
     out["update_iteration_convs_us"] = round(total * 1e3, 1)
     if args.no_lookup:
         print(json.dumps(out, indent=1))

@@ -35,8 +35,9 @@ __device__ __forceinline__ int swz(int row) { return (row >> 1) & 7; }
 
 constexpr int kTY = 4, kTX = 32;  // default tile: kTY rows x kTX columns
 
-// ablation build (tools/exp: -DOFLOW_ABLATE): exp_flags bits drop parts of the kernel to time the rest; the product
-// build compiles every test to false
+// ablation build (tools/exp: -DOFLOW_ABLATE): exp_flags bits drop parts of the kernel to time the rest (2 MFMAs, 4 A
+// staging writes, 8 instance-norm partials, 16 epilogue stores, 32 B staging writes, 64 the main loop's per-step
+// barrier); the product build compiles every test to false
 #ifdef OFLOW_ABLATE
 #define OFLOW_ABL(bit) ((a.exp_flags & (bit)) != 0)
 #else
@@ -298,7 +299,7 @@ __global__ __launch_bounds__(64 * WM * WN, WM * WN == 8 ? 1 : 2) void conv_s32_k
       RB[s_] = __builtin_amdgcn_raw_buffer_load_b128(rsB, boff[s_], (STEP) * a.npad * 128, 0);                      \
   }
 #define OFLOW_WRITE_B(RB, BUF)                                                                                       \
-  _Pragma("unroll") for (int s_ = 0; s_ < BPER; ++s_) {                                                              \
+  if (!OFLOW_ABL(32)) _Pragma("unroll") for (int s_ = 0; s_ < BPER; ++s_) {                                          \
     const int item = tid + s_ * NTH;                                                                            \
     const int n = item >> 3, c = item & 7;                                                                           \
     if (BITEMS % NTH == 0 || item < BITEMS)                                                                     \
@@ -441,7 +442,7 @@ __global__ __launch_bounds__(64 * WM * WN, WM * WN == 8 ? 1 : 2) void conv_s32_k
           OFLOW_LOAD_A(ra, g2);
         }
       }
-      __syncthreads(); /* B(i+1) [A] visible; every read of step i done before step i+1 overwrites its buffers */
+      if (!OFLOW_ABL(64)) __syncthreads(); /* B(i+1) [A] visible; every read of step i done before step i+1 overwrites its buffers */
       // 6-7
       OFLOW_READ_OPS(xah, xal, xbh, xbl, i_ + 1, 0);
       OFLOW_MFMAS(yah, yal, ybh, ybl);
@@ -617,6 +618,7 @@ __global__ __launch_bounds__(64 * WM * WN, WM * WN == 8 ? 1 : 2) void conv_s32_k
     if ((a.y0 == nullptr && a.fn == nullptr) || OFLOW_ABL(16)) return;
   }
 
+  if (OFLOW_ABL(16)) return;
   // S32 / GRU consumers: one thread = one pixel x 8 consecutive channels, KIT items per thread. The GRU state operands
   // of every item (h; z) are loaded first, all in flight at once, then consumed: one memory round trip per epilogue
   // instead of one per item.
