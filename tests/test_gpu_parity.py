@@ -275,6 +275,31 @@ def test_warp_bilinear_staged_and_direct_tiles(sigma, pad, width):
         _warp_close(got, ref, (sigma, pad, ac))
 
 
+@pytest.mark.parametrize("c,h,w,sigma", [(1, 77, 132, 8.0), (3, 436, 1024, 8.0), (4, 50, 64, 20.0), (3, 70, 64, 20.0), (2, 33, 200, 0.0),
+                                           (3, 130, 96, 60.0)])
+@pytest.mark.parametrize("pad", ["zeros", "border", "reflection"])
+def test_warp_strip_kernel_equals_tile_kernel(c, h, w, sigma, pad):
+    """The strip-walking warp (64-column strips, 16-row steps, an LDS ring of +-28 px; taps outside it gathered from
+    global memory: sigma 20 / 60) = the per-tile staged kernel (oflow_exp_set_warp_strip(0)), bit for bit; ragged
+    heights (segments ending mid-step), C = 1..4, the SURVEY warp workload's frame size; and = the oracle."""
+    import ctypes
+    g = torch.Generator().manual_seed(c * 1000 + h)
+    img = (torch.rand(2, c, h, w, generator=g) * 255).floor()
+    px = torch.from_numpy(synthetic.hash_normal(13 + c, (2, 2, h, w), sigma)) if sigma > 0 else torch.zeros(2, 2, h, w)
+    flow = oop.normalize(px)
+    lib = _native.load()
+    lib.oflow_exp_set_warp_strip.argtypes = [ctypes.c_int]
+    outs = []
+    for on in (1, 0):
+        lib.oflow_exp_set_warp_strip(on)
+        try:
+            outs.append(optical_flow.warp(img.to(DEV), flow.to(DEV), "bilinear", pad, False).cpu())
+        finally:
+            lib.oflow_exp_set_warp_strip(1)
+    assert torch.equal(outs[0], outs[1])
+    _warp_close(outs[0], oop.warp(img, flow, "bilinear", pad, False), (c, h, w, sigma, pad))
+
+
 def test_grid_sample_and_bilinear_sampler_match_oracle():
     img = torch.from_numpy(synthetic.hash_normal(8, (6, 3, 20, 30), 1.0))
     coords = torch.from_numpy(synthetic.hash_normal(9, (6, 7, 5, 2), 12.0)) + 12.0

@@ -1,6 +1,7 @@
 """In-process A/B of the LDS-staged warp's channels per workgroup (oflow_exp_set_warp_cpw: 0 = all channels in one
 workgroup, 1 = one workgroup per channel, ...) on the SURVEY warp workload (8, 3, 436, 1024), flow normalize(N(0, 8^2))
-px i.i.d. plus a smooth and a zero flow; outputs compared bit for bit across the settings. Prints JSON lines."""
+px i.i.d. plus a smooth and a zero flow; outputs compared bit for bit across the settings. HOOK / CPW select another
+hook and its settings (HOOK=oflow_exp_set_warp_strip CPW=1,0: strip-walking vs per-tile kernel). Prints JSON lines."""
 import ctypes
 import json
 import os
@@ -22,7 +23,8 @@ DEV = torch.device("cuda", 0)
 
 def main():
     lib = N.load()
-    lib.oflow_exp_set_warp_cpw.argtypes = [ctypes.c_int]
+    hook = getattr(lib, os.environ.get("HOOK", "oflow_exp_set_warp_cpw"))  # e.g. HOOK=oflow_exp_set_warp_strip CPW=1,0
+    hook.argtypes = [ctypes.c_int]
     b, c, h, w = 8, 3, 436, 1024
     flows = {}
     flows["iid8"] = [optical_flow.normalize(torch.from_numpy(synthetic.hash_normal(5 + k, (b, 2, h, w), 8.0))).to(DEV) for k in range(2)]
@@ -37,11 +39,11 @@ def main():
         for name, fl in flows.items():
             res, outs = {}, {}
             for cpw in settings:
-                lib.oflow_exp_set_warp_cpw(cpw)
+                hook(cpw)
                 outs[cpw] = optical_flow.warp(frames[0], fl[0]).clone()
             for _ in range(3):
                 for cpw in settings:
-                    lib.oflow_exp_set_warp_cpw(cpw)
+                    hook(cpw)
                     ts = []
                     for i in range(20):
                         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -51,7 +53,7 @@ def main():
                         torch.cuda.synchronize()
                         ts.append(e0.elapsed_time(e1) * 1e3)
                     res.setdefault(cpw, []).append(statistics.median(ts))
-            lib.oflow_exp_set_warp_cpw(0)
+            hook(settings[0])
             same = all(torch.equal(outs[settings[0]], outs[k]) for k in settings)
             print(json.dumps({"flow": name, "bit_identical": same,
                               **{f"cpw{k}_us": round(min(v), 2) for k, v in res.items()},

@@ -15,6 +15,7 @@
 // Other modes, and frames whose rows are not 16-B multiples: one thread per output pixel, flow read and output
 // writes coalesced along W; the gathered taps of neighbouring lanes are neighbours too for smooth flow.
 #include <algorithm>
+#include <type_traits>
 
 #include "oflow_internal.h"
 
@@ -392,6 +393,191 @@ __global__ __launch_bounds__(kWThreads) void warp_bilinear_lds_kernel(WarpArgs a
   }
 }
 
+// Warp fast path (flow given, bilinear, C <= 3, 16-B frame rows): a workgroup walks down a 64-column strip of one
+// image in 16-row steps and keeps the source rows its taps can reach in an LDS ring: rows y - kSM .. y + 16 + kSM and
+// columns x0 - kSM .. x0 + 64 + kSM of every channel (kSM = 28 px: |flow| of an i.i.d. N(0, 8^2) field stays inside for
+// all but ~0.1 % of pixels). Each step brings in only the 16 new rows (loaded one step ahead into registers), so every
+// source byte is read ~1.9x from L2 (the strip's side margins and a segment's first rows) instead of ~8x with per-tile
+// bounding boxes, and with coalesced 16-B row reads. Taps outside the ring (a larger flow) are gathered from global
+// memory by that lane. Same arithmetic as grid_warp_kernel: bit-identical results.
+constexpr int kSThreads = 1024, kSWaves = kSThreads / 64;
+constexpr int kSX = 64, kSY = 16, kSM = 28;           // strip width, rows per step, margin
+constexpr int kSRows = kSY / kSWaves;                 // output rows per thread per step
+constexpr int kSR = 2 * kSY + 2 * kSM;                // ring rows (88: one step of slack, see the loop)
+constexpr int kSC = kSX + 2 * kSM;                    // ring columns (120 = 30 float4)
+constexpr int kSC4 = kSC / 4;
+constexpr int kSMaxC = 3;
+constexpr int kSPre = (kSY * kSC4 * kSMaxC + kSThreads - 1) / kSThreads;  // float4 of a step's new rows per thread
+
+__global__ __launch_bounds__(kSThreads) void warp_strip_kernel(WarpArgs a, int strips, int segs, int seg_h) {
+  __shared__ __attribute__((aligned(16))) float sRing[kSMaxC * kSR * kSC];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  // XCD-aware order: block ids equal mod 8 share an L2; each XCD takes a contiguous run of (image, strip, segment)
+  const int nwg = gridDim.x, q8 = nwg / 8, r8 = nwg % 8, xcd = blockIdx.x % 8;
+  int t = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + blockIdx.x / 8;
+  const int seg = t % segs;
+  t /= segs;
+  const int strip = t % strips;
+  const int b = t / strips;
+  const int C = a.C, H = a.H, W = a.W, HW = H * W;
+  const int x0 = strip * kSX, xb = x0 - kSM;
+  const int ys = seg * seg_h, ye = min(H, ys + seg_h);
+  const float* __restrict__ src = a.frame + (size_t)b * C * HW;
+  float* __restrict__ dst = a.out + (size_t)b * C * HW;
+  const float* __restrict__ fxp = a.flow + (size_t)(2 * b) * HW;
+  const float* __restrict__ fyp = a.flow + (size_t)(2 * b + 1) * HW;
+
+  // one float4 of image row yy (ring slot yy mod kSR), column chunk j, channel c; rows / chunks outside the image: 0
+  auto fetch = [&](int c, int yy, int j) {
+    const int xx = xb + 4 * j;
+    if (yy >= 0 && yy < H && xx >= 0 && xx < W)
+      return *reinterpret_cast<const float4*>(src + (size_t)c * HW + (size_t)yy * W + xx);
+    return make_float4(0.f, 0.f, 0.f, 0.f);
+  };
+  auto put = [&](int c, int yy, int j, float4 v) {
+    const int slot = ((yy % kSR) + kSR) % kSR;
+    *reinterpret_cast<float4*>(&sRing[(c * kSR + slot) * kSC + 4 * j]) = v;
+  };
+  // rows [y, y + kSY) of every channel: item e -> (c, row, chunk)
+  const int nitems = C * kSY * kSC4;
+  // a step's new rows are loaded kSD steps ahead into one of kSD register sets (static index: the step loop is
+  // unrolled kSD times), so each load has kSD steps of work to land behind
+  constexpr int kSD = 3;
+  float4 pre[kSD][kSPre];
+  auto load_rows = [&](float4 (&dst)[kSPre], int y) {
+#pragma unroll
+    for (int k = 0; k < kSPre; ++k) {
+      const int e = tid + k * kSThreads;
+      const int c = e / (kSY * kSC4), rem = e - c * (kSY * kSC4);
+      const int rr = rem / kSC4, j = rem - rr * kSC4;
+      dst[k] = e < nitems ? fetch(c, y + rr, j) : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+  };
+  auto store_rows = [&](const float4 (&v)[kSPre], int y) {
+#pragma unroll
+    for (int k = 0; k < kSPre; ++k) {
+      const int e = tid + k * kSThreads;
+      const int c = e / (kSY * kSC4), rem = e - c * (kSY * kSC4);
+      const int rr = rem / kSC4, j = rem - rr * kSC4;
+      if (e < nitems) put(c, y + rr, j, v[k]);
+    }
+  };
+  // prologue: the first step's kSR rows (ys - kSM ..): every load issued before the first LDS store; then the next
+  // step's new rows in registers
+  {
+    constexpr int R0 = kSY + 2 * kSM;  // the first step's rows
+    constexpr int NP = (R0 * kSC4 * kSMaxC + kSThreads - 1) / kSThreads;
+    const int ni = C * R0 * kSC4;
+    float4 pv[NP];
+#pragma unroll
+    for (int k = 0; k < NP; ++k) {
+      const int e = tid + k * kSThreads;
+      const int c = e / (R0 * kSC4), rem = e - c * (R0 * kSC4);
+      const int rr = rem / kSC4, j = rem - rr * kSC4;
+      pv[k] = e < ni ? fetch(c, ys - kSM + rr, j) : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+#pragma unroll
+    for (int k = 0; k < NP; ++k) {
+      const int e = tid + k * kSThreads;
+      const int c = e / (R0 * kSC4), rem = e - c * (R0 * kSC4);
+      const int rr = rem / kSC4, j = rem - rr * kSC4;
+      if (e < ni) put(c, ys - kSM + rr, j, pv[k]);
+    }
+  }
+  // new rows of steps 1 .. kSD (step k needs rows ys + k*kSY + kSM .. + kSY - 1), set k % kSD
+#pragma unroll
+  for (int k = 1; k <= kSD; ++k) load_rows(pre[k % kSD], ys + k * kSY + kSM);
+  const int xo = x0 + lane;
+  // the step's flow (wave w: rows y + w + kSWaves * h), loaded one step ahead
+  float fl[kSRows][2];
+  auto load_flow = [&](int y) {
+#pragma unroll
+    for (int h = 0; h < kSRows; ++h) {
+      const int yo = min(y + wave + kSWaves * h, H - 1), xc = min(xo, W - 1);
+      fl[h][0] = fxp[yo * W + xc];
+      fl[h][1] = fyp[yo * W + xc];
+    }
+  };
+  load_flow(ys);
+
+  // one step at row y; Q = the register set holding step y + kSY's new rows (refilled with step y + (kSD+1)*kSY's)
+  // One barrier per step: the ring holds one step of slack (kSR = the 72 rows a step reads + 16), so the rows step
+  // s + 1 adds (y + kSY + kSM ..) go to the slots of rows y - kSY - kSM .., which step s - 1 read last: after this
+  // step's barrier they are free, and the barrier of step s + 1 publishes them.
+  auto step = [&](int y, auto Qc) -> bool {
+    constexpr int Q = decltype(Qc)::value;
+    if (y >= ye) return false;
+    __syncthreads();
+    if (y + kSY < ye) {
+      store_rows(pre[Q], y + kSY + kSM);
+      load_rows(pre[Q], y + (kSD + 1) * kSY + kSM);
+    }
+    float cur[kSRows][2];
+#pragma unroll
+    for (int h = 0; h < kSRows; ++h) {
+      cur[h][0] = fl[h][0];
+      cur[h][1] = fl[h][1];
+    }
+    if (y + kSY < ye) load_flow(y + kSY);
+    // ---- the step's 16 rows: wave w takes rows y + w + kSWaves * h ----
+#pragma unroll
+    for (int h = 0; h < kSRows; ++h) {
+      const int yo = y + wave + kSWaves * h;
+      if (yo < ye && xo < W) {
+        const int pix = yo * W + xo;
+        const float gx = linspace_m1_p1(xo, W) + cur[h][0];
+        const float gy = linspace_m1_p1(yo, H) + cur[h][1];
+        const float ix = pad_coord(unnormalize(gx, W, a.ac), W, a.pad, a.ac);
+        const float iy = pad_coord(unnormalize(gy, H, a.ac), H, a.pad, a.ac);
+        const float fx = floorf(ix), fy = floorf(iy);
+        const int tx0 = to_index(fx), ty0 = to_index(fy);
+        const float wx = ix - fx, wy = iy - fy;
+        const float ex = 1.0f - wx, ey = 1.0f - wy;
+        const float nw = ey * ex, ne = ey * wx, sw = wy * ex, se = wy * wx;
+        const unsigned m = (inb(tx0, ty0, W, H) ? 1u : 0u) | (inb(tx0 + 1, ty0, W, H) ? 2u : 0u) |
+                           (inb(tx0, ty0 + 1, W, H) ? 4u : 0u) | (inb(tx0 + 1, ty0 + 1, W, H) ? 8u : 0u);
+        // every tap read lies in the ring: rows y - kSM .. y + kSY + kSM - 1, columns xb .. xb + kSC - 1
+        const int ylo = (m & 3u) ? ty0 : ty0 + 1, yhi = (m & 12u) ? ty0 + 1 : ty0;
+        const int xlo = (m & 5u) ? tx0 : tx0 + 1, xhi = (m & 10u) ? tx0 + 1 : tx0;
+        const bool ring = m == 0u || (ylo >= y - kSM && yhi < y + kSY + kSM && xlo >= xb && xhi < xb + kSC);
+        if (ring) {
+          // every channel's taps read before any is combined (C <= kSMaxC: a static loop)
+          const int s0 = ((ty0 % kSR) + kSR) % kSR, s1 = s0 + 1 == kSR ? 0 : s0 + 1;
+          const int cx = tx0 - xb;
+          float v[kSMaxC][4];
+#pragma unroll
+          for (int c = 0; c < kSMaxC; ++c) {
+            const float* r0 = sRing + (c * kSR + s0) * kSC + cx;
+            const float* r1 = sRing + (c * kSR + s1) * kSC + cx;
+            const bool ok = c < C;
+            v[c][0] = (ok && (m & 1u)) ? r0[0] : 0.f;
+            v[c][1] = (ok && (m & 2u)) ? r0[1] : 0.f;
+            v[c][2] = (ok && (m & 4u)) ? r1[0] : 0.f;
+            v[c][3] = (ok && (m & 8u)) ? r1[1] : 0.f;
+          }
+#pragma unroll
+          for (int c = 0; c < kSMaxC; ++c)
+            if (c < C) dst[(size_t)c * HW + pix] = bilerp(v[c], nw, ne, sw, se);
+        } else {
+          const int o = ty0 * W + tx0;
+          for (int c = 0; c < C; ++c) {
+            const float* sp = src + (size_t)c * HW + o;
+            const float v[4] = {(m & 1u) ? sp[0] : 0.f, (m & 2u) ? sp[1] : 0.f, (m & 4u) ? sp[W] : 0.f,
+                                (m & 8u) ? sp[W + 1] : 0.f};
+            dst[(size_t)c * HW + pix] = bilerp(v, nw, ne, sw, se);
+          }
+        }
+      }
+    }
+    return true;
+  };
+  for (int y = ys; y < ye; y += kSD * kSY) {
+    if (!step(y, std::integral_constant<int, 1>{})) break;
+    if (!step(y + kSY, std::integral_constant<int, 2>{})) break;
+    if (!step(y + 2 * kSY, std::integral_constant<int, 0>{})) break;
+  }
+}
+
 }  // namespace
 }  // namespace oflow
 
@@ -399,6 +585,7 @@ using namespace oflow;
 
 namespace {
 int g_warp_cpw = 0;  // channels per staged-tile workgroup (0: all; experiment hook oflow_exp_set_warp_cpw)
+int g_warp_strip = 1;  // warp (flow given) on the strip-walking kernel (0: the per-tile boxes; oflow_exp_set_warp_strip)
 
 template <bool FLOW>
 int launch_warp(const WarpArgs& a, int mode, hipStream_t s) {
@@ -411,6 +598,20 @@ int launch_warp(const WarpArgs& a, int mode, hipStream_t s) {
       const int tiles_x = (a.Wo + kWTX - 1) / kWTX, tiles_y = (a.Ho + kWTY - 1) / kWTY;
       const int cpw = g_warp_cpw > 0 ? std::min(g_warp_cpw, a.C) : a.C;
       const long long nb = (long long)a.B * tiles_x * tiles_y * ((a.C + cpw - 1) / cpw);
+      if (FLOW && g_warp_strip && a.C <= kSMaxC && (a.W & 3) == 0 && (reinterpret_cast<uintptr_t>(a.frame) & 15) == 0 &&
+          a.W >= kSX && a.H >= 2 * kSY && a.W < 32768 && a.H < 32768) {
+        // strip walk: one round of at most one workgroup per CU (256 CUs; 135 KB of LDS each), segments >= 8 steps
+        const int strips = (a.W + kSX - 1) / kSX;
+        const long long cols = (long long)a.B * strips;
+        int segs = static_cast<int>(std::max(1ll, std::min(256 / cols, (long long)a.H / (8 * kSY))));
+        const int seg_h = (((a.H + segs - 1) / segs) + kSY - 1) / kSY * kSY;
+        segs = (a.H + seg_h - 1) / seg_h;
+        if (cols * segs < (1ll << 31)) {
+          hipLaunchKernelGGL(warp_strip_kernel, dim3(static_cast<unsigned>(cols * segs)), dim3(kSThreads), 0, s, a,
+                             strips, segs, seg_h);
+          break;
+        }
+      }
       if ((a.W & 3) == 0 && (reinterpret_cast<uintptr_t>(a.frame) & 15) == 0 && a.W < 32768 && a.H < 32768 &&
           nb < (1ll << 31)) {
         hipLaunchKernelGGL((warp_bilinear_lds_kernel<FLOW>), dim3(static_cast<unsigned>(nb)), dim3(kWThreads), 0, s, a,
@@ -457,3 +658,4 @@ extern "C" int oflow_grid_sample_f32(const float* d_input, const float* d_grid, 
 
 // experiment hook (not part of include/oflow.h): channels per LDS-staged warp workgroup (0 = all of the frame's)
 extern "C" void oflow_exp_set_warp_cpw(int cpw) { g_warp_cpw = cpw; }
+extern "C" void oflow_exp_set_warp_strip(int on) { g_warp_strip = on; }
