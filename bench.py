@@ -91,10 +91,12 @@ def warp_leg(dev, reps: int = 20):
     ms = mean_ms(evs)
     nbytes = (2 * c + 2) * 4 * b * h * w
     ach = nbytes / (ms * 1e-3) / 1e9
-    return {"note": "optical_flow.warp (HIP grid_warp, bilinear/border/align_corners=False) on frame (8, 3, 436, 1024), "
-                    "flow normalize(N(0, 8^2) px), timed after the timed region; not part of the RAFT step",
+    return {"note": "optical_flow.warp (HIP warp_strip kernel, bilinear/border/align_corners=False) on frame "
+                    "(8, 3, 436, 1024), flow normalize(N(0, 8^2) px), timed after the timed region; not part of the "
+                    "RAFT step",
             "bound": "hbm", "launch_ms": round(ms, 5), "launches": reps, "algorithmic_bytes_per_launch": nbytes,
-            "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4)}
+            "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4),
+            "traffic": pmc_traffic("sintel", 8, "warp")}
 
 
 def pyramid_cost(batch: int, dims, c: int = 256):
@@ -490,6 +492,15 @@ def main() -> int:
             "mfma": {"executed_f16_tflops": round(tf, 1), "peak_tflops": MFMA_F16_PEAK_TFLOPS,
                      "frac": round(tf / MFMA_F16_PEAK_TFLOPS, 4), "flops_per_launch": flops},
         }
+        # compound bound: the launch cannot be shorter than its real (PMC) HBM bytes at peak bandwidth, nor than its
+        # executed f16 MFMA work at the dense peak; frac = that bound / the measured launch time
+        trf = line["roofline"]["traffic"]
+        if trf:
+            t_hbm = trf / (HBM_PEAK_GBS * 1e9) * 1e6
+            t_mfma = flops / (MFMA_F16_PEAK_TFLOPS * 1e12) * 1e6
+            line["roofline"]["compound"] = {"bound_us": round(max(t_hbm, t_mfma), 2), "hbm_us": round(t_hbm, 2),
+                                            "mfma_us": round(t_mfma, 2),
+                                            "frac": round(max(t_hbm, t_mfma) / (lk_ms * 1e3), 4)}
         line["kernels"] = {}
         if pk:
             line["kernels"]["corr_pyramid"] = pyramid_entry(pk, ppg, dims, split=split_pyr)
