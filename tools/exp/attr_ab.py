@@ -37,6 +37,8 @@ def main():
         for attr, v in arms[k].items():
             if attr.startswith("lib:"):  # an experiment hook of the native library: lib:<symbol> = int argument
                 getattr(N.load(), attr[4:])(int(v))
+            elif attr.startswith("native:"):  # a module constant of optical_flow._native (e.g. a kernel threshold)
+                setattr(N, attr[7:], v)
             elif attr.startswith("bn:"):  # an update-block conv's output-channel block (model.update.CONV_BN)
                 from model import update as U
                 U.CONV_BN[attr[3:]] = int(v)
