@@ -39,6 +39,10 @@ def main():
                 getattr(N.load(), attr[4:])(int(v))
             elif attr.startswith("native:"):  # a module constant of optical_flow._native (e.g. a kernel threshold)
                 setattr(N, attr[7:], v)
+            elif attr.startswith("mod:"):  # mod:<module>.<name>, e.g. mod:model.extractor.FOLD_BLOCK0
+                import importlib
+                mname, _, name = attr[4:].rpartition(".")
+                setattr(importlib.import_module(mname), name, v)
             elif attr.startswith("bn:"):  # an update-block conv's output-channel block (model.update.CONV_BN)
                 from model import update as U
                 U.CONV_BN[attr[3:]] = int(v)
