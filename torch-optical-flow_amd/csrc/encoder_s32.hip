@@ -159,7 +159,8 @@ __global__ __launch_bounds__(64 * kStatWaves) void norm_stats_kernel(const float
   }
 }
 
-// one thread = one pixel x 8 channels
+// one thread = one pixel x 8 channels; every operand as 16-B loads (the per-channel affines too), 32-bit indexing
+// (the host checks P * C / 8 < 2^31)
 __global__ __launch_bounds__(256) void norm_apply_kernel(const float* __restrict__ x, int C, int B, int H, int W,
                                                          const float* __restrict__ alpha, const float* __restrict__ beta,
                                                          int act, int res_mode, const uint8_t* res, long long resps,
@@ -167,18 +168,20 @@ __global__ __launch_bounds__(256) void norm_apply_kernel(const float* __restrict
                                                          const float* __restrict__ beta2, int res_act, int s2d,
                                                          uint8_t* y, long long yps) {
   const int C8 = C / 8;
-  const long long P = (long long)B * H * W;
-  const long long item = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  const int HW = H * W, P = B * HW;
+  const int item = blockIdx.x * blockDim.x + threadIdx.x;
   if (item >= P * C8) return;
-  const int c8 = static_cast<int>(item % C8);
-  const long long p = item / C8;
-  const int b = static_cast<int>(p / ((long long)H * W));
+  const int p = item / C8, c8 = item - p * C8;
+  const int b = p / HW;
   const int c0 = c8 * 8;
-  const float4* xp = reinterpret_cast<const float4*>(x + p * C + c0);
-  const float4 u0 = xp[0], u1 = xp[1];
-  float v[8] = {u0.x, u0.y, u0.z, u0.w, u1.x, u1.y, u1.z, u1.w};
-  const float* al = alpha + (long long)b * C + c0;
-  const float* be = beta + (long long)b * C + c0;
+  auto ld8 = [](const float* q, float (&o)[8]) {
+    const float4 u0 = reinterpret_cast<const float4*>(q)[0], u1 = reinterpret_cast<const float4*>(q)[1];
+    o[0] = u0.x; o[1] = u0.y; o[2] = u0.z; o[3] = u0.w; o[4] = u1.x; o[5] = u1.y; o[6] = u1.z; o[7] = u1.w;
+  };
+  float v[8], al[8], be[8];
+  ld8(x + (long long)p * C + c0, v);
+  ld8(alpha + b * C + c0, al);
+  ld8(beta + b * C + c0, be);
 #pragma unroll
   for (int j = 0; j < 8; ++j) v[j] = act_fn(v[j] * al[j] + be[j], act);
   if (res_mode == 1) {  // S32 residual (identity shortcut)
@@ -188,11 +191,10 @@ __global__ __launch_bounds__(256) void norm_apply_kernel(const float* __restrict
     for (int j = 0; j < 8; ++j) v[j] = act_fn(v[j] + (static_cast<float>(rh[j]) + static_cast<float>(rlo[j])), res_act);
   } else if (res_mode >= 2) {  // normalised raw residual: 2 = the downsample branch norm3(conv1x1(x)); 3 = a block
                                 // input kept raw, relu(norm(x)) (the stem's output feeding layer1's first block)
-    const float4* rp = reinterpret_cast<const float4*>(x2 + p * C + c0);
-    const float4 r0 = rp[0], r1 = rp[1];
-    const float r[8] = {r0.x, r0.y, r0.z, r0.w, r1.x, r1.y, r1.z, r1.w};
-    const float* a2 = alpha2 + (long long)b * C + c0;
-    const float* b2 = beta2 + (long long)b * C + c0;
+    float r[8], a2[8], b2[8];
+    ld8(x2 + (long long)p * C + c0, r);
+    ld8(alpha2 + b * C + c0, a2);
+    ld8(beta2 + b * C + c0, b2);
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       float rn = r[j] * a2[j] + b2[j];
@@ -203,7 +205,7 @@ __global__ __launch_bounds__(256) void norm_apply_kernel(const float* __restrict
   long long pd = p;
   int cd = c0;
   if (s2d) {
-    const int pix = static_cast<int>(p - (long long)b * H * W);
+    const int pix = p - b * HW;
     const int yy = pix / W, xx = pix - yy * W;
     pd = ((long long)b * (H >> 1) + (yy >> 1)) * (W >> 1) + (xx >> 1);
     cd = c0 + ((yy & 1) * 2 + (xx & 1)) * C;
@@ -258,9 +260,11 @@ extern "C" int oflow_norm_apply_s32(const float* d_x, int C, int B, int H, int W
   if (res_mode >= 2 && (!d_x2 || !d_alpha2 || !d_beta2)) return OFLOW_E_NULL;
   if (s2d && ((H | W) & 1)) return OFLOW_E_SHAPE;
   if (((uintptr_t)d_x & 15) || ((uintptr_t)d_y & 15) || (y_pixel_stride & 127) ||
-      (d_res && (((uintptr_t)d_res & 15) || (res_pixel_stride & 127))) || (d_x2 && ((uintptr_t)d_x2 & 15)))
+      (d_res && (((uintptr_t)d_res & 15) || (res_pixel_stride & 127))) || (d_x2 && ((uintptr_t)d_x2 & 15)) ||
+      (((uintptr_t)d_alpha | (uintptr_t)d_beta) & 15) || (((uintptr_t)d_alpha2 | (uintptr_t)d_beta2) & 15))
     return OFLOW_E_ALIGN;
   const long long items = (long long)B * H * W * (C / 8);
+  if (items >= (1ll << 31)) return OFLOW_E_SHAPE;  // 32-bit indexing in the kernel
   hipLaunchKernelGGL(norm_apply_kernel, dim3((unsigned)((items + 255) / 256)), dim3(256), 0, static_cast<hipStream_t>(stream),
                      d_x, C, B, H, W, d_alpha, d_beta, activation, res_mode, static_cast<const uint8_t*>(d_res),
                      res_pixel_stride, d_x2, d_alpha2, d_beta2, res_activation, s2d, static_cast<uint8_t*>(d_y),
