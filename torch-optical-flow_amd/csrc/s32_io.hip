@@ -39,14 +39,15 @@ __device__ __forceinline__ void put8(uint8_t* line, const float* v) {
 __global__ __launch_bounds__(256) void pack_s32_kernel(const float* __restrict__ x, long long xbs, int C, int B, int HW,
                                                        int act, int yc0, uint8_t* y0, long long y0ps, uint8_t* y1,
                                                        long long y1ps, float* f, int fcs) {
-  const long long P = (long long)B * HW;
+  // 32-bit indexing (the host checks P * C8 < 2^31): 64-bit divisions dominated these memory-bound kernels
+  const int P = B * HW;
   const int C8 = (C + 7) / 8;
-  const long long item = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  const int item = blockIdx.x * blockDim.x + threadIdx.x;
   if (item >= P * C8) return;
-  const int c8 = static_cast<int>(item / P);
-  const long long p = item - (long long)c8 * P;
-  const int b = static_cast<int>(p / HW);
-  const int pix = static_cast<int>(p - (long long)b * HW);
+  const int c8 = item / P;
+  const long long p = item - c8 * P;
+  const int b = static_cast<int>(p) / HW;
+  const int pix = static_cast<int>(p) - b * HW;
   const int c0 = c8 * 8;
   float v[8];
 #pragma unroll
@@ -71,14 +72,14 @@ __global__ __launch_bounds__(256) void flow_prep_kernel(const float* __restrict_
                                                         uint8_t* pm, uint8_t* d0, long long d0ps, uint8_t* d1,
                                                         long long d1ps) {
   constexpr int KS = 7, R = 3, G = 4;
-  const long long HW = (long long)H * W;
-  const long long P = B * HW;
-  const long long item = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  const int HW = H * W;
+  const int P = B * HW;  // 32-bit indexing: the host checks P * G < 2^31
+  const int item = blockIdx.x * blockDim.x + threadIdx.x;
   if (item >= P * G) return;
-  const int g = static_cast<int>(item % G);
+  const int g = item % G;
   const long long p = item / G;
-  const int b = static_cast<int>(p / HW);
-  const int pix = static_cast<int>(p - b * HW);
+  const int b = static_cast<int>(p) / HW;
+  const int pix = static_cast<int>(p) - b * HW;
   const int y = pix / W, x = pix - y * W;
   const float* cx = coords + (long long)b * 2 * HW;
   const float* cy = cx + HW;
@@ -218,6 +219,7 @@ extern "C" int oflow_pack_s32_f32(const float* d_x, long long x_batch_stride, in
   if ((y0_pixel_stride & 127) || ((uintptr_t)d_y0 & 15) || (d_y1 && ((y1_pixel_stride & 127) || ((uintptr_t)d_y1 & 15))))
     return OFLOW_E_ALIGN;
   const long long items = (long long)B * H * W * ((C + 7) / 8);
+  if (items >= (1ll << 31)) return OFLOW_E_SHAPE;  // 32-bit indexing in the kernel
   hipLaunchKernelGGL(pack_s32_kernel, dim3((unsigned)((items + 255) / 256)), dim3(256), 0, static_cast<hipStream_t>(stream),
                      d_x, x_batch_stride, C, B, H * W, activation, dst_channel, static_cast<uint8_t*>(d_y0), y0_pixel_stride,
                      static_cast<uint8_t*>(d_y1), y1_pixel_stride, d_nhwc, nhwc_pixel_stride);
@@ -232,6 +234,7 @@ extern "C" int oflow_flow_prep_s32(const float* d_coords, int B, int H, int W, v
   if (((uintptr_t)d_patches & 15) || (d_flow0 && ((uintptr_t)d_flow0 & 3)) || (d_flow1 && ((uintptr_t)d_flow1 & 3)))
     return OFLOW_E_ALIGN;
   const long long items = (long long)B * H * W * 4;
+  if (items >= (1ll << 31)) return OFLOW_E_SHAPE;  // 32-bit indexing in the kernel
   hipLaunchKernelGGL(flow_prep_kernel, dim3((unsigned)((items + 255) / 256)), dim3(256), 0, static_cast<hipStream_t>(stream),
                      d_coords, B, H, W, static_cast<uint8_t*>(d_patches), static_cast<uint8_t*>(d_flow0),
                      flow0_pixel_stride, static_cast<uint8_t*>(d_flow1), flow1_pixel_stride);
