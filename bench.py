@@ -10,11 +10,15 @@ resident in rank 0's HBM), every rank pads -> RAFT forward -> unpads, flows are 
 N = 1 there is no collective. Synthetic frames (integer texture, known shift) and hash-generated weights: no
 dataset or checkpoint is reachable offline.
 
+Inputs: the 8 pairs of the reference-generated golden batch (tests/golden/raft_e2e_batch.npz: 'sintel8' / 'kitti8',
+synthetic frames the repository's generator rebuilds bit for bit), tiled to the global batch.
+
 Printed (rank 0, one JSON line): pairs/s for the whole job, the lookup kernel's roofline (algorithmic bytes per
-launch / mean launch time from HIP events recorded on the launch stream inside the timed region), the corr
-pyramid kernel's MFMA rate, ``epe_vs_reference`` (the benchmarked model on the reference's own golden pair, run
-in this process before timing), and the oracle (PyTorch-CPU restatement) timed on this host's cores on the
-workload's per-GPU batch. ``--pairs-per-gpu 1 --iters 24`` is predict.py's batch-1 latency case.
+launch / mean launch time from HIP events recorded on the launch stream inside the timed region), ``roofline.step``
+(the whole step's executed f16 MFMA rate against the dense peak, counted per launch in one extra untimed forward),
+the corr pyramid kernel's MFMA rate, ``epe_vs_reference`` (the LAST TIMED STEP's flows for the golden batch's pairs
+against the reference's own flows for them), and the oracle (PyTorch-CPU restatement) timed on this host's cores on
+the workload's per-GPU batch. ``--pairs-per-gpu 1 --iters 24`` is predict.py's batch-1 latency case.
 """
 from __future__ import annotations
 
@@ -39,6 +43,9 @@ HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 MFMA_F32_PEAK_TFLOPS = 157.3  # dense fp32 MFMA (v_mfma_f32_32x32x2_f32), spec
 MFMA_F16_PEAK_TFLOPS = 2500.0  # dense fp16 MFMA, spec (no sparsity)
 PMC_TRAFFIC_FILE = os.path.join(REPO, "profiles", "lookup_traffic.json")
+BATCH_GOLDEN = os.path.join(REPO, "tests", "golden", "raft_e2e_batch.npz")
+# the reference forward's FLOPs per pair (12 iterations, measured with the torch profiler)
+REF_GFLOP_PER_PAIR = {"sintel": 735.9, "kitti": 767.6}
 
 WORKLOADS = {
     # name: (pairs per GPU, H, W, iters, padder mode, alternate_corr)           BASELINE.json configs[...]
@@ -96,7 +103,8 @@ def warp_leg(dev, reps: int = 20):
                     "RAFT step",
             "bound": "hbm", "launch_ms": round(ms, 5), "launches": reps, "algorithmic_bytes_per_launch": nbytes,
             "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4),
-            "traffic": pmc_traffic("sintel", 8, "warp")}
+            "traffic": pmc_traffic("sintel", 8, "warp"),
+            "frac_traffic": frac_on_traffic(pmc_traffic("sintel", 8, "warp"), ms)}
 
 
 def pyramid_cost(batch: int, dims, c: int = 256):
@@ -142,6 +150,7 @@ def lookup_api_leg(ppg: int, dims, flow_low, dev, reps: int = 12):
         "bound": "hbm", "launch_ms": round(ms, 5), "launches": len(ts), "algorithmic_bytes_per_launch": nbytes,
         "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4),
         "traffic": pmc_traffic("sintel" if h0 == 55 else "kitti", ppg, "corr_lookup_api"),
+        "frac_traffic": frac_on_traffic(pmc_traffic("sintel" if h0 == 55 else "kitti", ppg, "corr_lookup_api"), ms),
     }
 
 
@@ -170,6 +179,14 @@ def pmc_traffic(workload: str, ppg: int, kernel: str):
     with open(PMC_TRAFFIC_FILE) as f:
         tr = json.load(f).get(f"{workload}:{ppg}:{kernel}")
     return tr.get("hbm_bytes_per_launch") if tr else None
+
+
+def frac_on_traffic(traffic, launch_ms: float):
+    """The launch's real HBM bytes (PMC, per launch) / its measured time, as a fraction of the HBM peak; None without
+    PMC data."""
+    if not traffic:
+        return None
+    return round(traffic / (launch_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
 
 
 def pyramid_entry(pk, ppg: int, dims, split: bool = False):
@@ -262,10 +279,48 @@ def cpu_baseline(h: int, w: int, iters: int, pairs: int):
     }
 
 
+def batch_golden(workload: str, h: int, w: int, iters: int):
+    """(tag, fixture) of the reference-generated batch golden matching this workload's frame size and iterations, or
+    (None, None): 'sintel8' / 'kitti8' (tests/golden/gen_goldens.py BATCH_CASES: 8 pairs, 12 iterations)."""
+    import numpy as np
+
+    tag = {"sintel": "sintel8", "kitti": "kitti8"}.get(workload)
+    if tag is None or not os.path.exists(BATCH_GOLDEN):
+        return None, None
+    g = np.load(BATCH_GOLDEN, allow_pickle=False)
+    b, gh, gw, giters, s, seed = (int(v) for v in g[f"{tag}_cfg"])
+    if (gh, gw, giters) != (h, w, iters):
+        return None, None
+    return tag, g
+
+
+def step_epe(out, tag: str, g, n_pairs: int):
+    """EPE of the timed step's own flows (``out`` = (flow_low, flow_up) of the last timed step, the global batch on
+    rank 0) for its first ``n_pairs`` pairs -- which are the golden batch's pairs -- against the reference's flows."""
+    b, h, w, iters, s, seed = (int(v) for v in g[f"{tag}_cfg"])
+    n = min(n_pairs, b)
+    low = out[0][:n].float().cpu()
+    up = out[1][:n, :, ::s, ::s].float().cpu()
+    el = torch.norm(low - torch.from_numpy(g[f"{tag}_low"][:n]), dim=1)
+    eu = torch.norm(up - torch.from_numpy(g[f"{tag}_up"][:n]), dim=1)
+    return {
+        "case": f"golden '{tag}': the last timed step's flows for its first {n} pair(s) ({h}x{w}, {iters} iters; "
+                f"the benchmarked batch's own pairs) vs the reference PyTorch-CPU flows for the same pairs",
+        "pairs": n,
+        "low_mean": float(el.mean()),
+        "low_max": float(el.max()),
+        "up_mean": float(eu.mean()),
+        "up_max": float(eu.max()),
+        "unit": "px",
+        "tolerance": "mean <= 1e-4, max <= 1e-3 px (SURVEY §8(c))",
+    }
+
+
 def golden_epe(model, dev, workload: str):
     """The reference's own flow for a golden pair (tests/golden/raft_e2e.npz, produced by the reference on CPU) vs this
     build's forward with the same weights, run through the benchmarked model before timing: EPE of the 1/8-res flow
-    and of the (strided) full-res flow."""
+    and of the (strided) full-res flow. Used where no batch golden matches the workload (hd, other iteration
+    counts)."""
     import numpy as np
 
     from model import InputPadder, synthetic
@@ -307,6 +362,8 @@ def main() -> int:
                     help="replay each rank's forward from a HIP graph (model/graph.py: one launch per step)")
     ap.add_argument("--no-conv-benchmark", action="store_true",
                     help="disable torch.backends.cudnn.benchmark (MIOpen exhaustive find of the conv algorithms)")
+    ap.add_argument("--range-guard", default=None, choices=["sync", "deferred", "off"],
+                    help="RAFT.range_guard (default: the model's, 'sync'); 'deferred' checks once after the timed region")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -334,6 +391,8 @@ def main() -> int:
     model.load_state_dict(synthetic.synthetic_state_dict(model.state_dict()))
     model = model.to(dev)
     model.update_impl = args.update_impl
+    if args.range_guard:
+        model.range_guard = args.range_guard
 
     img0 = img1 = None
     if args.workload == "corr":  # configs[1]: fmaps (B, 256, 128, 128) ~ N(0, 1.45^2), coords = grid + N(0, 4^2)
@@ -351,14 +410,19 @@ def main() -> int:
                 out = cb(cgrid)
             return out, out
 
-    elif rank == 0:  # two distinct pairs tiled to the global batch, resident in rank 0's HBM
-        a0, a1 = synthetic.synthetic_pair(2, h, w, seed=0)
-        reps = -(-global_batch // 2)
+    gtag, gfix = batch_golden(args.workload, h, w, iters) if args.workload != "corr" and not alt else (None, None)
+    if args.workload != "corr" and rank == 0:
+        # the golden batch's pairs (8 distinct pairs for sintel / kitti), tiled to the global batch, in rank 0's HBM
+        npairs = int(gfix[f"{gtag}_cfg"][0]) if gtag else 2
+        seed = int(gfix[f"{gtag}_cfg"][5]) if gtag else 0
+        a0, a1 = synthetic.synthetic_pair(npairs, h, w, seed=seed)
+        reps = -(-global_batch // npairs)
         img0 = a0.to(dev).repeat(reps, 1, 1, 1)[:global_batch].contiguous()
         img1 = a1.to(dev).repeat(reps, 1, 1, 1)[:global_batch].contiguous()
     padder = InputPadder((h, w), mode=pmode or "sintel")
     dims = _native.pyramid_dims((h + 7) // 8, (w + 7) // 8, 4)
-    epe = golden_epe(model, dev, args.workload) if args.workload != "corr" and rank == 0 else None
+    # without a batch golden for this workload: the 1-pair golden through the benchmarked model, before timing
+    epe = golden_epe(model, dev, args.workload) if args.workload != "corr" and rank == 0 and not gtag else None
     shard_shape = (global_batch, 3, h, w)
     flow_shapes = ((2, dims[0][0], dims[0][1]), (2, h, w))
 
@@ -406,6 +470,20 @@ def main() -> int:
             dist.barrier()
         elapsed = time.perf_counter() - t0
         _native.set_event_recorder(None)
+        if getattr(model, "range_guard", "off") == "deferred":
+            model.check_range(dev)  # every timed forward's split operands were in range
+        if rank == 0 and gtag:
+            epe = step_epe(out, gtag, gfix, global_batch)
+        # one more (untimed) forward with the per-launch flop counter: the step roofline
+        step_flops = None
+        if args.workload != "corr" and not args.graph:
+            cnt = {}
+            _native.set_flop_counter(cnt)
+            fwd(img0[:ppg] if img0 is not None else torch.zeros((ppg, 3, h, w), device=dev),
+                img1[:ppg] if img1 is not None else torch.zeros((ppg, 3, h, w), device=dev))
+            _native.set_flop_counter(None)
+            torch.cuda.synchronize(dev)
+            step_flops = cnt
 
     # the RAFT forward builds its pyramid from split-fp16 features (split encoders + CorrBlock); the "corr" workload
     # calls the CorrBlock API (fp32 MFMA pyramid)
@@ -486,6 +564,7 @@ def main() -> int:
             "unit": "GB/s",
             "frac": round(ach / HBM_PEAK_GBS, 4),
             "traffic": pmc_traffic(args.workload, ppg, "corr_lookup_convc1"),
+            "frac_traffic": frac_on_traffic(pmc_traffic(args.workload, ppg, "corr_lookup_convc1"), lk_ms),
             "algorithmic_bytes_per_launch": lk_bytes,
             "launch_ms": round(lk_ms, 5),
             "launches": len(lk),
@@ -531,6 +610,31 @@ def main() -> int:
         }
         if pk:
             line["kernels"] = {"corr_pyramid": pyramid_entry(pk, ppg, dims, split=split_pyr)}
+    if step_flops and step_flops.get("exec_f16"):
+        # whole-step roofline: per GPU, the flops one forward over this rank's ppg pairs issues, over the step time
+        sec = elapsed / args.steps
+        ex, us = step_flops["exec_f16"], step_flops["useful"]
+        ref = REF_GFLOP_PER_PAIR.get(args.workload)
+        step = {
+            "note": "per GPU: matrix-core flops of one forward over the rank's pairs (counted per launch in an untimed "
+                    "forward) / ms_per_step; executed = the f16 MFMAs issued (3 split products, channel padding to "
+                    "32-channel groups and output blocks included); useful = fp32-equivalent flops of the layers' real "
+                    "channels as executed (after Q11's skipped mask heads and the hoisted GRU context term)",
+            "executed_f16_flops": ex,
+            "executed_f16_tflops": round(ex / sec / 1e12, 1),
+            "peak_tflops": MFMA_F16_PEAK_TFLOPS,
+            "frac": round(ex / sec / 1e12 / MFMA_F16_PEAK_TFLOPS, 4),
+            "useful_fp32eq_flops": us,
+            "useful_fp32eq_gflop_per_pair": round(us / ppg / 1e9, 1),
+            "useful_fp32eq_tflops": round(us / sec / 1e12, 1),
+            "fma_f32_flops": step_flops.get("fma_f32", 0),
+        }
+        if ref and h == WORKLOADS[args.workload][1]:
+            rt = ref * 1e9 * ppg / sec / 1e12
+            step["reference_gflop_per_pair"] = ref
+            step["reference_equivalent_tflops"] = round(rt, 1)
+            step["reference_equivalent_frac_of_fp32_mfma"] = round(rt / MFMA_F32_PEAK_TFLOPS, 4)
+        line.setdefault("roofline", {})["step"] = step
     if epe is not None:
         line["epe_vs_reference"] = {k: (round(v, 8) if isinstance(v, float) else v) for k, v in epe.items()}
     if rank == 0 and not args.no_cpu_baseline and args.workload in ("sintel", "kitti"):

@@ -195,6 +195,12 @@ int oflow_flow_prep_s32(const float* d_coords, int B, int H, int W, void* d_patc
  * coords (B, 2, H, W) fp32 in place (raft.py:133 `coords1 = coords1 + delta_flow`), from an S32 input of in_groups
  * groups (1..8): fp32 FMAs on the exact S32 values; d_weight (2, C, 3, 3) fp32 as the nn.Conv2d stores it, d_bias [2].
  * Built for small grids (one image at 1/8 resolution); larger ones run faster as oflow_conv_s32 with n_pad 32. */
+/* oflow_set_range_flag: register d_flag (one unsigned int in device memory of the current device; NULL: off) as the
+ * range flag of the split-fp16 operands. Every kernel that writes or stages S32 values (the conv epilogues and staging,
+ * norm_apply, pack / flow_prep, the fused lookup + convc1) sets it to 1 (atomic or) when a value's hi half overflows
+ * fp16 (|x| >= 65520 or inf); it is never cleared by the library. Synchronous (a copy to each kernel module's symbol). */
+int oflow_set_range_flag(unsigned int* d_flag);
+
 int oflow_flow_head2_s32(const void* d_x, long long x_pixel_stride, int in_groups, const float* d_weight,
                          const float* d_bias, int B, int H, int W, float* d_coords, void* stream);
 /* oflow_corr_lookup_tiled_nhwc_f32: the tiled lookup as fp32 NHWC rows [B*H*W][row_floats] (d_out 16-B aligned) in the

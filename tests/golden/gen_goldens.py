@@ -10,7 +10,7 @@ written. Bytecode writing is disabled so the read-only tree stays untouched.
 Inputs come from the repository's own deterministic generators (``model/synthetic.py``), which the GPU box
 re-runs bit-for-bit; fmaps are therefore not stored, only a float64 checksum that the tests re-verify.
 
-Usage:  python tests/golden/gen_goldens.py [corr] [warp] [raft] [io]   (default: all)
+Usage:  python tests/golden/gen_goldens.py [corr] [warp] [raft] [batch] [io]   (default: all)
 """
 from __future__ import annotations
 
@@ -181,6 +181,41 @@ def gen_raft(RAFT, InputPadder) -> None:
     np.savez_compressed(os.path.join(HERE, "raft_e2e.npz"), **out)
 
 
+BATCH_CASES = {
+    # the benchmarked configurations themselves (bench.py WORKLOADS "sintel" / "kitti": 8 pairs per GPU, 12 iters,
+    # 'sintel' padding): at 8 pairs the update loop runs on two pair lanes and the flow head's output conv on the
+    # split MFMA kernel (above FLOW_HEAD2_MAX_PIXELS), the path the bench times
+    "sintel8": dict(B=8, H=436, W=1024, iters=12, stride=8, mode="sintel", seed=0),
+    "kitti8": dict(B=8, H=375, W=1242, iters=12, stride=8, mode="sintel", seed=5),
+}
+
+
+def gen_raft_batch(RAFT, InputPadder) -> None:
+    """RAFT forward(test_mode=True) at the benchmarked batch (`raft.py:87-147`), written to raft_e2e_batch.npz: the
+    full 1/8-res flow and the full-res flow at stride 8, per pair."""
+    torch.set_num_threads(max(1, os.cpu_count() or 1))
+    model = RAFT()
+    model.load_state_dict(synthetic.synthetic_state_dict(model.state_dict()))
+    model.eval()
+    out = {}
+    with torch.inference_mode():
+        for tag, c in BATCH_CASES.items():
+            img0, img1 = synthetic.synthetic_pair(c["B"], c["H"], c["W"], seed=c["seed"])
+            padder = InputPadder(img0.shape, mode=c["mode"])
+            p0, p1 = padder.pad(img0, img1)
+            low, up = model(p0, p1, iters=c["iters"], test_mode=True)
+            up = padder.unpad(up)
+            s = c["stride"]
+            out[f"{tag}_cfg"] = np.array([c["B"], c["H"], c["W"], c["iters"], s, c["seed"]], dtype=np.int64)
+            out[f"{tag}_mode"] = np.array(c["mode"])
+            out[f"{tag}_low"] = low.numpy()
+            out[f"{tag}_up"] = up[..., ::s, ::s].contiguous().numpy()
+            out[f"{tag}_up_checksum"] = _checksum(up)
+            out[f"{tag}_img_checksum"] = np.stack([_checksum(img0), _checksum(img1)])
+            print(tag, "flow_up mean |f| =", float(up.norm(dim=1).mean()), flush=True)
+    np.savez_compressed(os.path.join(HERE, "raft_e2e_batch.npz"), **out)
+
+
 def io_flows():
     """Flow fields of the I/O goldens, from the repository's own generators (the tests rebuild them)."""
     flows = {
@@ -244,13 +279,15 @@ def main() -> int:
         print("gen_goldens: /root/reference absent; fixtures are committed, nothing to do")
         return 0
     RAFT, CorrBlock, InputPadder, bilinear_sampler, coords_grid, ref_operator = _import_reference()
-    which = sys.argv[1:] or ["corr", "warp", "raft", "io"]
+    which = sys.argv[1:] or ["corr", "warp", "raft", "batch", "io"]
     if "corr" in which:
         gen_corr(CorrBlock, coords_grid)
     if "warp" in which:
         gen_warp(ref_operator)
     if "raft" in which:
         gen_raft(RAFT, InputPadder)
+    if "batch" in which:
+        gen_raft_batch(RAFT, InputPadder)
     if "io" in which:
         gen_io()
     return 0

@@ -446,3 +446,45 @@ def test_fmap_gradient_gemms_match_fp64(b, c, n):
     bound2 = torch.bmm(f1.double().abs().view(b, c, n), G.abs()) * s
     assert bool(((g1.cpu().double().view(b, c, n) - r1).abs() <= 2e-5 * bound1 + 1e-6).all())
     assert bool(((g2.cpu().double().view(b, c, n) - r2).abs() <= 2e-5 * bound2 + 1e-6).all())
+
+
+@pytest.mark.parametrize("ac", [False, True])
+@pytest.mark.parametrize("pad", ["border", "reflection", "zeros"])
+def test_grid_sample_bicubic_far_out_grid_backward(pad, ac):
+    """Bicubic backward with grid values of about +-1e7 (tap coordinates far past 2^20): under border / reflection
+    padding every tap is padded from its float coordinate, so the input gradient lands on the border / reflected pixels
+    as ATen's grid_sampler_2d_backward puts it (the forward samples those pixels too); zeros padding drops them."""
+    g = torch.Generator().manual_seed(17)
+    x = torch.randn(1, 3, 9, 12, generator=g)
+    grid = torch.rand(1, 6, 7, 2, generator=g) * 2.0 - 1.0
+    grid[0, :3, :, 0] = 1e7
+    grid[0, 3:, :4, 1] = -1e7
+    grid[0, 5, 6] = torch.tensor([-3e7, 2e7])
+    r = torch.randn(1, 3, 6, 7, generator=g)
+    a_x = x.clone().requires_grad_()
+    (torch.nn.functional.grid_sample(a_x, grid, mode="bicubic", padding_mode=pad, align_corners=ac) * r).sum().backward()
+    d_x = x.to(DEV).requires_grad_()
+    out = torch.ops.oflow.grid_sample(d_x, grid.to(DEV), _native.INTERP["bicubic"], _native.PADDING[pad], ac)
+    (out * r.to(DEV)).sum().backward()
+    ref = a_x.grad
+    assert float(ref.abs().max()) > 0 or pad == "zeros"
+    assert float((d_x.grad.cpu() - ref).abs().max()) <= 1e-5 * float(ref.abs().max()) + 1e-5
+
+
+def test_warp_backward_forms_only_the_wanted_gradient():
+    """needs_input_grad reaches the native backward (output_mask): a frame without gradient gets no frame gradient
+    (no zero fill, no atomics), and the flow gradient equals the one computed with both outputs."""
+    img0, _ = synthetic.synthetic_pair(1, 24, 40, seed=3)
+    flow = oop.normalize(torch.from_numpy(synthetic.hash_normal(15, (1, 2, 24, 40), 4.0)))
+    r = torch.from_numpy(synthetic.hash_normal(16, (1, 3, 24, 40), 1.0)).to(DEV)
+    f = img0.to(DEV)
+    w1 = flow.to(DEV).requires_grad_()
+    (optical_flow.warp(f, w1) * r).sum().backward()
+    f2, w2 = f.clone().requires_grad_(), flow.to(DEV).requires_grad_()
+    (optical_flow.warp(f2, w2) * r).sum().backward()
+    assert torch.equal(w1.grad, w2.grad)
+    go = r.contiguous()
+    gf, gw = torch.ops.oflow.grid_warp_backward(go, f, w1.detach(), 0, 1, False, [False, True])
+    assert gf.numel() == 0 and torch.equal(gw, w2.grad)
+    gf, gw = torch.ops.oflow.grid_warp_backward(go, f, w1.detach(), 0, 1, False, [True, False])
+    assert gw.numel() == 0 and torch.allclose(gf, f2.grad, rtol=1e-5, atol=1e-5)  # fp32 atomics: order varies

@@ -50,6 +50,35 @@ def test_raft_matches_reference_flows(golden, tag, impl):
     assert xl <= 1e-3 and xu <= 1e-3, (xl, xu)
 
 
+@pytest.mark.parametrize("tag", ["sintel8", "kitti8"])
+def test_raft_matches_reference_flows_at_benchmarked_batch(golden, tag):
+    """The forward bench.py times (8 pairs per GPU, 12 iterations, 'sintel' padding, default model: split encoders,
+    split-fp16 pyramid, lookup fused into convc1, two pair lanes, the flow head's output conv on the split MFMA kernel)
+    against the reference's own flows for the same 8 pairs (tests/golden/raft_e2e_batch.npz), every pair."""
+    from optical_flow import _native
+
+    g = golden("raft_e2e_batch")
+    b, h, w, iters, s, seed = (int(v) for v in g[f"{tag}_cfg"])
+    img0, img1 = synthetic.synthetic_pair(b, h, w, seed=seed)
+    chk = np.stack([[float(x.double().sum()), float((x.double() ** 2).sum()), float(x.abs().max())] for x in (img0, img1)])
+    assert np.array_equal(chk, g[f"{tag}_img_checksum"])
+    padder = InputPadder(img0.shape, mode=str(g[f"{tag}_mode"]))
+    p0, p1 = (x.to(DEV) for x in padder.pad(img0, img1))
+    model = _model(RAFT)
+    assert model.pair_lanes == 2 and model.update_impl == "split" and model.encoder_impl == "split"
+    lh, lw = p0.shape[-2] // 8, p0.shape[-1] // 8
+    assert b * lh * lw > _native.FLOW_HEAD2_MAX_PIXELS  # the conv flow head, not the small-grid FMA kernel
+    with torch.inference_mode():
+        low, up = model(p0, p1, iters=iters, test_mode=True)
+    up = padder.unpad(up)[..., ::s, ::s]
+    for k in range(b):
+        ml, xl = _epe(low[k : k + 1], g[f"{tag}_low"][k : k + 1])
+        mu, xu = _epe(up[k : k + 1], g[f"{tag}_up"][k : k + 1])
+        print(f"{tag} pair {k}: low EPE mean {ml:.2e} max {xl:.2e}; up EPE mean {mu:.2e} max {xu:.2e}")
+        assert ml <= 1e-4 and mu <= 1e-4, (k, ml, mu)
+        assert xl <= 1e-3 and xu <= 1e-3, (k, xl, xu)
+
+
 def test_product_matches_oracle_on_gpu():
     """Same GPU convolutions, HIP correlation vs ATen correlation: isolates the kernels' contribution."""
     img0, img1 = synthetic.synthetic_pair(2, 436, 1024, seed=1)
@@ -315,3 +344,44 @@ def test_graphed_forward_equals_eager():
             lo_e, up_e = model(a, b, iters=24, test_mode=True)
             lo_g, up_g = g(a, b)
             assert torch.equal(lo_g, lo_e) and torch.equal(up_g, up_e)
+
+
+@pytest.mark.parametrize("where", ["images", "convc1", "convc2"])
+def test_range_guard_raises_on_split_overflow(where):
+    """The split-fp16 range guard (oflow_set_range_flag): an activation whose fp16 hi half overflows (|x| >= 65520) sets
+    the device flag inside the kernel that splits it, and the forward raises RuntimeError -- with no per-convolution
+    check. Injected three ways: huge input frames (cnet's stem output, batch norm folded), convc1 weights x 1e6 (the
+    fused lookup + convc1 epilogue), convc2 weights x 1e6 (a conv_s32 epilogue's S32 store). A normal forward
+    afterwards runs (the flag was cleared) and matches its earlier output bit for bit."""
+    img0, img1 = synthetic.synthetic_pair(2, 128, 160, seed=6)
+    p0, p1 = img0.to(DEV), img1.to(DEV)
+    model = _model(RAFT)
+    with torch.inference_mode():
+        ref = model(p0, p1, iters=4, test_mode=True)
+    bad = _model(RAFT)
+    a0, a1 = p0, p1
+    if where == "images":
+        a0, a1 = p0 * 1e6, p1 * 1e6
+    else:
+        w = getattr(bad.update_block.encoder, where).weight
+        with torch.no_grad():
+            w.mul_(1e6)
+        bad.invalidate_weight_caches()
+    with torch.inference_mode():
+        with pytest.raises(RuntimeError, match="fp16 range"):
+            bad(a0, a1, iters=4, test_mode=True)
+        got = model(p0, p1, iters=4, test_mode=True)  # flag cleared: a valid forward does not raise
+    assert torch.equal(got[0], ref[0]) and torch.equal(got[1], ref[1])
+
+
+def test_range_guard_deferred_mode():
+    """range_guard = "deferred": the forward does not wait for the flag; check_range() (or a later forward that finds
+    the GPU past the earlier one) raises."""
+    img0, img1 = synthetic.synthetic_pair(1, 128, 160, seed=6)
+    bad = _model(RAFT)
+    bad.range_guard = "deferred"
+    with torch.inference_mode():
+        bad(img0.to(DEV) * 1e6, img1.to(DEV) * 1e6, iters=2, test_mode=True)
+        with pytest.raises(RuntimeError, match="fp16 range"):
+            bad.check_range()
+        bad.check_range()  # cleared

@@ -116,3 +116,34 @@ def test_raft_forward_matches_reference(golden, tag):
     epe_up = oraft.end_point_error(up, torch.from_numpy(g[f"{tag}_up"]))
     assert float(epe_low.mean()) <= 1e-4 and float(epe_low.max()) <= 1e-3
     assert float(epe_up.mean()) <= 1e-4 and float(epe_up.max()) <= 1e-3
+
+
+@pytest.mark.parametrize("tag,pair", [("sintel8", 7), ("kitti8", 3)])
+def test_batch_goldens_are_per_pair_reference_flows(golden, tag, pair):
+    """raft_e2e_batch.npz (the benchmarked 8-pair batches, made by the reference itself): the frames are the
+    repository's generator output (input checksums), and pair k of the batch equals the oracle's forward of that
+    pair alone (synthetic_pair seeds pair k with seed + k) -- pairs are independent, so the batch golden pins every
+    pair of the GPU's batched forward."""
+    g = golden("raft_e2e_batch")
+    b, h, w, iters, s, seed = (int(v) for v in g[f"{tag}_cfg"])
+    assert b == 8 and iters == 12
+    img0, img1 = synthetic.synthetic_pair(1, h, w, seed=seed + pair)
+    model = oraft.RAFT().eval()
+    model.load_state_dict(synthetic.synthetic_state_dict(model.state_dict()))
+    padder = oraft.InputPadder(img0.shape, mode=str(g[f"{tag}_mode"]))
+    with torch.inference_mode():
+        low, up = model(*padder.pad(img0, img1), iters=iters, test_mode=True)
+    up = padder.unpad(up)[..., ::s, ::s]
+    epe_low = oraft.end_point_error(low, torch.from_numpy(g[f"{tag}_low"][pair : pair + 1]))
+    epe_up = oraft.end_point_error(up, torch.from_numpy(g[f"{tag}_up"][pair : pair + 1]))
+    assert float(epe_low.mean()) <= 1e-4 and float(epe_low.max()) <= 1e-3
+    assert float(epe_up.mean()) <= 1e-4 and float(epe_up.max()) <= 1e-3
+
+
+def test_batch_golden_input_checksums(golden):
+    g = golden("raft_e2e_batch")
+    for tag in ("sintel8", "kitti8"):
+        b, h, w, iters, s, seed = (int(v) for v in g[f"{tag}_cfg"])
+        img0, img1 = synthetic.synthetic_pair(b, h, w, seed=seed)
+        chk = np.stack([[float(x.double().sum()), float((x.double() ** 2).sum()), float(x.abs().max())] for x in (img0, img1)])
+        assert np.array_equal(chk, g[f"{tag}_img_checksum"]), tag

@@ -119,21 +119,45 @@ def test_shard_bounds_cover_batch():
 
 
 def _shape_worker(rank, world, port, q):
+    """Rank 0 holds 3 pairs but every rank is told (4, 3, 16, 24): the one-time collective check raises on every
+    rank. Then, after a step with the right shape, rank 0's batch changes: rank 0 raises after completing the
+    collectives with NaN pieces; the peers return (NaN shard / no flows) instead of blocking."""
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        img = torch.zeros(3, 3, 16, 24)
+        out = []
+        src_img = torch.zeros(3, 3, 16, 24) if rank == 0 else None
         try:
-            scatter_pairs(img, img, torch.device("cpu"), shape=(4, 3, 16, 24))
-            q.put((rank, False))
+            scatter_pairs(src_img, src_img, torch.device("cpu"), shape=(4, 3, 16, 24))
+            out.append("no-error")
         except ValueError:
-            q.put((rank, True))
+            out.append("ValueError")
+        good = torch.ones(4, 3, 16, 24) if rank == 0 else None
+        s0, _ = scatter_pairs(good, good, torch.device("cpu"), shape=(4, 3, 16, 24))
+        out.append("ok" if bool((s0 == 1).all()) else "bad")
+        bad = torch.ones(5, 3, 16, 24) if rank == 0 else None  # changed after the check
+        try:
+            s0, _ = scatter_pairs(bad, bad, torch.device("cpu"), shape=(4, 3, 16, 24))
+            out.append("nan" if bool(torch.isnan(s0).all()) else "values")
+        except ValueError:
+            out.append("ValueError")
+        try:
+            low, up = infer_sharded(_fake_forward, bad, bad, torch.device("cpu"), shape=(4, 3, 16, 24),
+                                    flow_shapes=((2, 2, 3), (2, 16, 24)))
+            out.append("none" if low is None and up is None else "flows")
+        except ValueError:
+            out.append("ValueError")
+        q.put((rank, tuple(out)))
     finally:
         dist.destroy_process_group()
 
 
-def test_scatter_refuses_a_shape_that_disagrees_with_the_batch():
-    """A caller-given global shape is checked against the source batch on the source rank (host-only, before any
-    collective): a mismatch raises instead of mis-sizing the scatter."""
-    res = _run(_shape_worker, 1)
-    assert res == [(0, True)]
+@pytest.mark.parametrize("world", [1, 2])
+def test_scatter_refuses_a_shape_that_disagrees_with_the_batch(world):
+    """A caller-given global shape that disagrees with the source batch fails on every rank (one-time collective
+    check), and a later change of the source batch fails on the source without leaving a peer blocked in a
+    collective (the test's queue timeout would catch a hang)."""
+    res = sorted(_run(_shape_worker, world))
+    assert res[0] == (0, ("ValueError", "ok", "ValueError", "ValueError"))
+    for r in res[1:]:
+        assert r[1] == ("ValueError", "ok", "nan", "none"), r

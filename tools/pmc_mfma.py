@@ -1,0 +1,81 @@
+"""Summarise tools/pmc_mfma_job.sh: per MFMA kernel of the step (name with template arguments + grid size), the median per
+dispatch of its counters and the derived matrix-core figures.
+
+    python tools/pmc_mfma.py <pass1 counter_collection.csv> <pass2 counter_collection.csv> [--json out.json]
+
+Derived (MI355X_MICROARCH.md: SQ_VALU_MFMA_BUSY_CYCLES counts SIMD cycles, 32 per 32x32x16 f16 MFMA; SQ_WAVE_CYCLES /
+SQ_WAIT_* / SQ_ACTIVE_INST_* count quad-cycles; GRBM_GUI_ACTIVE is summed over the 8 XCDs):
+  clock_ghz     = GRBM_GUI_ACTIVE / 8 / duration
+  mfma_util     = SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE / 8 * 1024 SIMDs)   (fraction of SIMD-cycles busy on MFMA)
+  busy_per_mfma = SQ_VALU_MFMA_BUSY_CYCLES / SQ_INSTS_MFMA   (32 expected for 32x32x16 f16)
+  wait_any / wait_inst / active = SQ_WAIT_ANY / SQ_WAIT_INST_ANY / SQ_ACTIVE_INST_ANY over SQ_WAVE_CYCLES
+  lds_conflict  = SQ_LDS_BANK_CONFLICT / SQ_LDS_IDX_ACTIVE
+Durations come from the PMC run's dispatch timestamps (dispatches serialised: each kernel alone).
+"""
+import argparse
+import csv
+import json
+import re
+import statistics
+from collections import defaultdict
+
+
+def short_name(k: str) -> str:
+    m = re.search(r"(\w+_kernel(?:<[^()]*>)?)", k)
+    return m.group(1).replace(" ", "") if m else k[:80]
+
+
+def load(path):
+    per = defaultdict(dict)  # (kernel, grid, dispatch) -> counter -> value ; "_dur_ns"
+    for r in csv.DictReader(open(path)):
+        key = (short_name(r["Kernel_Name"]), int(r["Grid_Size"]), r["Dispatch_Id"])
+        d = per[key]
+        d[r["Counter_Name"]] = d.get(r["Counter_Name"], 0.0) + float(r["Counter_Value"])
+        d["_dur_ns"] = float(r["End_Timestamp"]) - float(r["Start_Timestamp"])
+    return per
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("paths", nargs="+")
+    ap.add_argument("--json", default=None)
+    a = ap.parse_args()
+    groups = defaultdict(lambda: defaultdict(list))  # (kernel, grid) -> counter -> [per-dispatch values]
+    for p in a.paths:
+        for (k, g, _), d in load(p).items():
+            for c, v in d.items():
+                groups[(k, g)][c].append(v)
+    out = []
+    for (k, g), cs in sorted(groups.items(), key=lambda kv: -statistics.median(kv[1]["_dur_ns"]) * len(kv[1]["_dur_ns"])):
+        med = {c: statistics.median(v) for c, v in cs.items()}
+        row = {"kernel": k, "grid": g, "dispatches": len(cs["_dur_ns"]), "us": round(med["_dur_ns"] / 1e3, 2)}
+        gui = med.get("GRBM_GUI_ACTIVE")
+        if gui:
+            row["clock_ghz"] = round(gui / 8 / med["_dur_ns"], 3)
+            if "SQ_VALU_MFMA_BUSY_CYCLES" in med:
+                row["mfma_util"] = round(med["SQ_VALU_MFMA_BUSY_CYCLES"] / (gui / 8 * 1024), 4)
+        if med.get("SQ_INSTS_MFMA"):
+            row["mfma_insts"] = med["SQ_INSTS_MFMA"]
+            if "SQ_VALU_MFMA_BUSY_CYCLES" in med:
+                row["busy_per_mfma"] = round(med["SQ_VALU_MFMA_BUSY_CYCLES"] / med["SQ_INSTS_MFMA"], 2)
+        wc = med.get("SQ_WAVE_CYCLES")
+        if wc:
+            for c, nm in (("SQ_WAIT_ANY", "wait_any"), ("SQ_WAIT_INST_ANY", "wait_inst"), ("SQ_ACTIVE_INST_ANY", "active"),
+                          ("SQ_WAIT_INST_LDS", "wait_inst_lds")):
+                if c in med:
+                    row[nm] = round(med[c] / wc, 4)
+        if med.get("SQ_LDS_IDX_ACTIVE"):
+            row["lds_conflict"] = round(med.get("SQ_LDS_BANK_CONFLICT", 0.0) / med["SQ_LDS_IDX_ACTIVE"], 4)
+        for c in ("SQ_INSTS_VALU", "SQ_INSTS_LDS", "SQ_INSTS_VMEM", "SQ_INSTS_SALU", "SQ_WAVES"):
+            if c in med:
+                row[c] = med[c]
+        out.append(row)
+    for r in out:
+        print(json.dumps(r))
+    if a.json:
+        with open(a.json, "w") as f:
+            json.dump(out, f, indent=1)
+
+
+if __name__ == "__main__":
+    main()

@@ -3,6 +3,16 @@
 
 extern "C" int oflow_abi_version(void) { return OFLOW_ABI_VERSION; }
 
+// every translation unit that writes or stages split-fp16 operands gets the flag pointer (for the current device)
+extern "C" int oflow_set_range_flag(unsigned int* d_flag) {
+  using namespace oflow;
+  int st = range_flag_set_conv(d_flag);
+  if (st == 0) st = range_flag_set_encoder(d_flag);
+  if (st == 0) st = range_flag_set_s32io(d_flag);
+  if (st == 0) st = range_flag_set_convc1(d_flag);
+  return st;  // OFLOW_OK or a HIP error code (positive)
+}
+
 extern "C" const char* oflow_status_string(int status) {
   switch (status) {
     case OFLOW_OK: return "ok";

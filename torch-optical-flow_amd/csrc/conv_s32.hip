@@ -103,6 +103,7 @@ __device__ __forceinline__ float act_fn(float v, int act) {
 }
 
 __device__ __forceinline__ void split8(const float* v, half8& hi, half8& lo) {
+  range_guard8(v);
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
     _Float16 h_, l_;
@@ -123,6 +124,11 @@ __device__ __forceinline__ void store_s32(uint8_t* y, long long ps, long long P,
   } else {
     _Float16* hp = reinterpret_cast<_Float16*>(line);
     _Float16* lp = reinterpret_cast<_Float16*>(line + 64);
+    float m = 0.f;
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+      if (n + j < N) m = fmaxf(m, fabsf(v[j]));
+    range_guard(m);
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       if (n + j < N) {
@@ -261,15 +267,19 @@ __global__ __launch_bounds__(64 * WM * WN, WM * WN == 8 ? 1 : 2) void conv_s32_k
           const int pb_ = 2 * (p >> 5) * kImgCols + 2 * (p & 31);                                                    \
           const int4 ko_ = *reinterpret_cast<const int4*>(sKoff + (G) * 32 + 4 * c);                                 \
           const int kov_[4] = {ko_.x, ko_.y, ko_.z, ko_.w};                                                          \
+          float mx_ = 0.f;                                                                                           \
           _Pragma("unroll") for (int e_ = 0; e_ < 4; ++e_) {                                                         \
             const float v_ = sImg[kov_[e_] < 0 ? kImgZero : pb_ + kov_[e_]];                                         \
+            mx_ = fmaxf(mx_, fabsf(v_));                                                                             \
             _Float16 hv, lv;                                                                                         \
             split_f16(v_, hv, lv);                                                                                   \
             h4[e_] = hv;                                                                                             \
             l4[e_] = lv;                                                                                             \
           }                                                                                                          \
+          range_guard(mx_);                                                                                          \
         } else if (((aok >> s_) & 1u) && (AIN != kInF32 || (G) * 32 + 4 * c < a.cin)) {                             \
           const float* fv = reinterpret_cast<const float*>(&RA[s_]);                                                 \
+          float mx_ = 0.f;                                                                                           \
           _Pragma("unroll") for (int e_ = 0; e_ < 4; ++e_) {                                                         \
             float v_ = fv[e_];                                                                                       \
             if constexpr (AIN == kInF32Norm) {                                                                       \
@@ -277,11 +287,13 @@ __global__ __launch_bounds__(64 * WM * WN, WM * WN == 8 ? 1 : 2) void conv_s32_k
               v_ = v_ * af.x + af.y;                                                                                 \
               v_ = v_ < 0.f ? 0.f : v_;                                                                              \
             }                                                                                                        \
+            mx_ = fmaxf(mx_, fabsf(v_));                                                                             \
             _Float16 hv, lv;                                                                                         \
             split_f16(v_, hv, lv);                                                                                   \
             h4[e_] = hv;                                                                                             \
             l4[e_] = lv;                                                                                             \
           }                                                                                                          \
+          range_guard(mx_);                                                                                          \
         }                                                                                                            \
         uint8_t* rw_ = sA + (BUF) * A_BYTES + p * RS + (c & 1) * 8;                                                  \
         *reinterpret_cast<half4_*>(rw_ + (((c >> 1) ^ swz(p)) << 4)) = h4;                                           \
@@ -905,6 +917,7 @@ int build_conv_args(ConvArgs& a, const void* d_x, long long x_pixel_stride, int 
 }
 
 }  // namespace
+OFLOW_RANGE_FLAG_SETTER(conv)
 }  // namespace oflow
 
 using namespace oflow;
@@ -952,6 +965,8 @@ extern "C" int oflow_conv_s32_ex3(const void* d_x, long long x_pixel_stride, int
   a.ain = in_format;
   if (d_addend) {  // GRU epilogues only; 16-B aligned rows of >= N floats
     if (epilogue == 0) return OFLOW_E_MODE;
+    // the epilogue reads whole 8-float octets of every row: N a multiple of 8 keeps them inside the row
+    if (N % 8) return OFLOW_E_SHAPE;
     if (((uintptr_t)d_addend & 15) || (addend_pixel_stride & 3) || addend_pixel_stride < N) return OFLOW_E_ALIGN;
     a.add = d_addend;
     a.addps = addend_pixel_stride;

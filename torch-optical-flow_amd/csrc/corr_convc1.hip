@@ -262,6 +262,7 @@ __global__ __launch_bounds__(kNT, 2) void corr_convc1_kernel(C1Args a) {
             v[e] = bilinear4(p[j * RW + i], p[j * RW + i + 1], p[(j + 1) * RW + i], p[(j + 1) * RW + i + 1], w4);
           }
         }
+        range_guard8(v);
         half8 hi, lo;
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
@@ -342,16 +343,19 @@ __global__ __launch_bounds__(kNT, 2) void corr_convc1_kernel(C1Args a) {
     const float4 t1 = *reinterpret_cast<const float4*>(&sT[pl * TS + n + 4]);
     const float v[8] = {t0.x, t0.y, t0.z, t0.w, t1.x, t1.y, t1.z, t1.w};
     half8 hi, lo;
+    float mx = 0.f;
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       const float2 sb = sbv[j];
       float x = v[j] * sb.x + sb.y;
       x = x < 0.f ? 0.f : x;  // relu (update.py:120); NaN propagates like ATen
+      mx = fmaxf(mx, x);
       _Float16 h_, l_;
       split_f16(x, h_, l_);
       hi[j] = h_;
       lo[j] = l_;
     }
+    range_guard(mx);
     uint8_t* line = a.y + (long long)(q0 + pl) * a.yps + (n >> 5) * 128 + ((n & 31) >> 3) * 16;
     *reinterpret_cast<half8*>(line) = hi;
     *reinterpret_cast<half8*>(line + 64) = lo;
@@ -363,6 +367,7 @@ __global__ __launch_bounds__(kNT, 2) void corr_convc1_kernel(C1Args a) {
 unsigned long long* g_convc1_stamps = nullptr;  // diagnostics (experiment hook): per-workgroup clock stamps
 
 }  // namespace
+OFLOW_RANGE_FLAG_SETTER(convc1)
 }  // namespace oflow
 
 using namespace oflow;

@@ -26,6 +26,7 @@ __device__ __forceinline__ float act_fn(float v, int act) {
 }
 
 __device__ __forceinline__ void put8(uint8_t* line, const float* v) {
+  range_guard8(v);
   half8 hi, lo;
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
@@ -87,6 +88,7 @@ __global__ __launch_bounds__(256) void stem_patches_kernel(const float* __restri
       }
     }
     half8 h;
+    if (piece < 4) range_guard8(v);  // (the lo pieces split the same values)
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
       _Float16 h_, l_;
@@ -214,6 +216,7 @@ __global__ __launch_bounds__(256) void norm_apply_kernel(const float* __restrict
 }
 
 }  // namespace
+OFLOW_RANGE_FLAG_SETTER(encoder)
 }  // namespace oflow
 
 using namespace oflow;
@@ -264,7 +267,7 @@ extern "C" int oflow_norm_apply_s32(const float* d_x, int C, int B, int H, int W
       (((uintptr_t)d_alpha | (uintptr_t)d_beta) & 15) || (((uintptr_t)d_alpha2 | (uintptr_t)d_beta2) & 15))
     return OFLOW_E_ALIGN;
   const long long items = (long long)B * H * W * (C / 8);
-  if (items >= (1ll << 31)) return OFLOW_E_SHAPE;  // 32-bit indexing in the kernel
+  if ((items + 255) / 256 * 256 >= (1ll << 31)) return OFLOW_E_SHAPE;  // 32-bit indexing over the rounded-up grid
   hipLaunchKernelGGL(norm_apply_kernel, dim3((unsigned)((items + 255) / 256)), dim3(256), 0, static_cast<hipStream_t>(stream),
                      d_x, C, B, H, W, d_alpha, d_beta, activation, res_mode, static_cast<const uint8_t*>(d_res),
                      res_pixel_stride, d_x2, d_alpha2, d_beta2, res_activation, s2d, static_cast<uint8_t*>(d_y),

@@ -40,6 +40,32 @@ __device__ __forceinline__ void split_f16(float v, _Float16& hi, _Float16& lo) {
   lo = static_cast<_Float16>(v - static_cast<float>(a));
 }
 
+// Range guard of the split-fp16 operands (S32, include/oflow.h): a value whose hi half would overflow fp16 (|v| >= 65520
+// rounds to inf; inf included, NaN not) sets the device flag registered by oflow_set_range_flag (sticky; the host reads
+// it once per forward and raises). Every translation unit that splits holds its own copy of the flag pointer
+// (internal linkage); OFLOW_RANGE_FLAG_SETTER(name) defines that unit's setter, which oflow_set_range_flag calls.
+namespace {
+__device__ unsigned int* g_range_flag = nullptr;
+}
+__device__ __forceinline__ void range_guard(float max_abs) {
+  if (__builtin_expect(max_abs >= 65520.0f, 0)) {
+    unsigned int* f = g_range_flag;
+    if (f != nullptr) atomicOr(f, 1u);
+  }
+}
+__device__ __forceinline__ void range_guard8(const float* v) {
+  range_guard(fmaxf(fmaxf(fmaxf(fabsf(v[0]), fabsf(v[1])), fmaxf(fabsf(v[2]), fabsf(v[3]))),
+                    fmaxf(fmaxf(fabsf(v[4]), fabsf(v[5])), fmaxf(fabsf(v[6]), fabsf(v[7])))));
+}
+#define OFLOW_RANGE_FLAG_SETTER(name)                                                              \
+  int range_flag_set_##name(unsigned int* d_flag) {                                                \
+    return static_cast<int>(hipMemcpyToSymbol(HIP_SYMBOL(g_range_flag), &d_flag, sizeof(d_flag)));     \
+  }
+int range_flag_set_conv(unsigned int* d_flag);
+int range_flag_set_encoder(unsigned int* d_flag);
+int range_flag_set_s32io(unsigned int* d_flag);
+int range_flag_set_convc1(unsigned int* d_flag);
+
 // Bilinear tap of the lookup: nw*w.x + ne*w.y + sw*w.z + se*w.w in one fixed rounding order, shared by every lookup
 // kernel (corr_lookup.hip, corr_convc1.hip) so that they agree bit for bit.
 __device__ __forceinline__ float bilinear4(float nw, float ne, float sw, float se, float4 w) {

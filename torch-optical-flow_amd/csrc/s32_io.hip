@@ -22,6 +22,7 @@ __device__ __forceinline__ float act_fn(float v, int act) {
 }
 
 __device__ __forceinline__ void put8(uint8_t* line, const float* v) {
+  range_guard8(v);
   half8 hi, lo;
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
@@ -105,6 +106,7 @@ __global__ __launch_bounds__(256) void flow_prep_kernel(const float* __restrict_
   if (g == 0 && d0) {
     const float fx = cx[pix] - static_cast<float>(x), fy = cy[pix] - static_cast<float>(y);
     _Float16 hx, lx, hy, ly;
+    range_guard(fmaxf(fabsf(fx), fabsf(fy)));
     split_f16(fx, hx, lx);
     split_f16(fy, hy, ly);
     for (int d = 0; d < 2; ++d) {
@@ -206,6 +208,7 @@ __global__ __launch_bounds__(1024) void flow_head2_kernel(const uint8_t* __restr
 }
 
 }  // namespace
+OFLOW_RANGE_FLAG_SETTER(s32io)
 }  // namespace oflow
 
 using namespace oflow;
@@ -219,7 +222,7 @@ extern "C" int oflow_pack_s32_f32(const float* d_x, long long x_batch_stride, in
   if ((y0_pixel_stride & 127) || ((uintptr_t)d_y0 & 15) || (d_y1 && ((y1_pixel_stride & 127) || ((uintptr_t)d_y1 & 15))))
     return OFLOW_E_ALIGN;
   const long long items = (long long)B * H * W * ((C + 7) / 8);
-  if (items >= (1ll << 31)) return OFLOW_E_SHAPE;  // 32-bit indexing in the kernel
+  if ((items + 255) / 256 * 256 >= (1ll << 31)) return OFLOW_E_SHAPE;  // 32-bit indexing over the rounded-up grid
   hipLaunchKernelGGL(pack_s32_kernel, dim3((unsigned)((items + 255) / 256)), dim3(256), 0, static_cast<hipStream_t>(stream),
                      d_x, x_batch_stride, C, B, H * W, activation, dst_channel, static_cast<uint8_t*>(d_y0), y0_pixel_stride,
                      static_cast<uint8_t*>(d_y1), y1_pixel_stride, d_nhwc, nhwc_pixel_stride);
@@ -234,7 +237,7 @@ extern "C" int oflow_flow_prep_s32(const float* d_coords, int B, int H, int W, v
   if (((uintptr_t)d_patches & 15) || (d_flow0 && ((uintptr_t)d_flow0 & 3)) || (d_flow1 && ((uintptr_t)d_flow1 & 3)))
     return OFLOW_E_ALIGN;
   const long long items = (long long)B * H * W * 4;
-  if (items >= (1ll << 31)) return OFLOW_E_SHAPE;  // 32-bit indexing in the kernel
+  if ((items + 255) / 256 * 256 >= (1ll << 31)) return OFLOW_E_SHAPE;  // 32-bit indexing over the rounded-up grid
   hipLaunchKernelGGL(flow_prep_kernel, dim3((unsigned)((items + 255) / 256)), dim3(256), 0, static_cast<hipStream_t>(stream),
                      d_coords, B, H, W, static_cast<uint8_t*>(d_patches), static_cast<uint8_t*>(d_flow0),
                      flow0_pixel_stride, static_cast<uint8_t*>(d_flow1), flow1_pixel_stride);

@@ -17,8 +17,9 @@
 //   grid_sample(input, grid, mode, padding_mode, align_corners)   bilinear_sampler    (utils.py:64-80)
 //   corr_lookup_backward(grad_out, coords, radius, H0, W0, L)     transpose of corr_lookup (training, §8(f) row 3)
 //   corr_pyramid_backward(level_grads, fmap1, fmap2) -> (g1, g2)  pool transpose + two fp32-MFMA GEMMs
-//   grid_warp_backward(grad_out, frame, flow, mode, pad, ac) -> (grad_frame, grad_flow)     warp's autograd
-//   grid_sample_backward(grad_out, input, grid, mode, pad, ac) -> (grad_input, grad_grid)   grid_sample's autograd
+//   grid_warp_backward(grad_out, frame, flow, mode, pad, ac, mask) -> (grad_frame, grad_flow)     warp's autograd
+//   grid_sample_backward(grad_out, input, grid, mode, pad, ac, mask) -> (grad_input, grad_grid)   grid_sample's autograd
+#include <array>
 #include <torch/library.h>
 #include <ATen/ATen.h>
 #include <ATen/hip/HIPContext.h>
@@ -396,55 +397,68 @@ Tensor grid_sample_meta(const Tensor& input, const Tensor& grid, int64_t mode, i
 }
 
 // warp / grid_sample backward (warp_backward.hip): (grad_frame, grad_flow) / (grad_input, grad_grid)
+// output_mask (ATen grid_sampler_2d_backward's): an output not wanted is returned as an empty (0-element) tensor and
+// the kernel gets a null pointer for it (no zero fill, no atomics for grad_frame)
 std::tuple<Tensor, Tensor> grid_warp_backward_impl(const Tensor& gout, const Tensor& frame, const Tensor& flow,
-                                                   int64_t mode, int64_t pad, bool ac, bool run) {
+                                                   int64_t mode, int64_t pad, bool ac, std::array<bool, 2> mask, bool run) {
   const char* what = "warp backward";
   check_modes(mode, pad, what);
   check_warp(frame, flow, what);
   TORCH_CHECK(gout.sizes() == frame.sizes(), what, ": grad_out ", gout.sizes(), " must match the frame ", frame.sizes());
-  if (!run) return {at::empty(frame.sizes(), frame.options().dtype(at::kFloat)), at::empty(flow.sizes(), flow.options().dtype(at::kFloat))};
+  const auto fopt = frame.options().dtype(at::kFloat), lopt = flow.options().dtype(at::kFloat);
+  if (!run)
+    return {at::empty(mask[0] ? frame.sizes() : at::IntArrayRef{0}, fopt), at::empty(mask[1] ? flow.sizes() : at::IntArrayRef{0}, lopt)};
   Tensor go = gpu_f32(gout, "grad_out", what), fr = gpu_f32(frame, "frame", what), fl = gpu_f32(flow, "flow", what);
-  Tensor gfr = at::zeros_like(fr), gfl = at::empty_like(fl);
+  Tensor gfr = mask[0] ? at::zeros_like(fr) : at::empty({0}, fopt), gfl = mask[1] ? at::empty_like(fl) : at::empty({0}, lopt);
   if (fr.numel() == 0) return {gfr, gfl.zero_()};
+  if (!mask[0] && !mask[1]) return {gfr, gfl};
   c10::hip::HIPGuardMasqueradingAsCUDA g(fr.device());
   check_status(oflow_grid_warp_backward_f32(go.data_ptr<float>(), fr.data_ptr<float>(), fl.data_ptr<float>(), (int)fr.size(0),
                                             (int)fr.size(1), (int)fr.size(2), (int)fr.size(3), (int)mode, (int)pad, ac ? 1 : 0,
-                                            gfr.data_ptr<float>(), gfl.data_ptr<float>(), cur_stream()),
+                                            mask[0] ? gfr.data_ptr<float>() : nullptr,
+                                            mask[1] ? gfl.data_ptr<float>() : nullptr, cur_stream()),
                what);
   return {gfr, gfl};
 }
-std::tuple<Tensor, Tensor> grid_warp_backward_hip(const Tensor& go, const Tensor& fr, const Tensor& fl, int64_t m, int64_t p, bool ac) {
-  return grid_warp_backward_impl(go, fr, fl, m, p, ac, true);
+std::tuple<Tensor, Tensor> grid_warp_backward_hip(const Tensor& go, const Tensor& fr, const Tensor& fl, int64_t m, int64_t p, bool ac,
+                                                  std::array<bool, 2> mask) {
+  return grid_warp_backward_impl(go, fr, fl, m, p, ac, mask, true);
 }
-std::tuple<Tensor, Tensor> grid_warp_backward_meta(const Tensor& go, const Tensor& fr, const Tensor& fl, int64_t m, int64_t p, bool ac) {
-  return grid_warp_backward_impl(go, fr, fl, m, p, ac, false);
+std::tuple<Tensor, Tensor> grid_warp_backward_meta(const Tensor& go, const Tensor& fr, const Tensor& fl, int64_t m, int64_t p, bool ac,
+                                                   std::array<bool, 2> mask) {
+  return grid_warp_backward_impl(go, fr, fl, m, p, ac, mask, false);
 }
 
 std::tuple<Tensor, Tensor> grid_sample_backward_impl(const Tensor& gout, const Tensor& input, const Tensor& grid,
-                                                     int64_t mode, int64_t pad, bool ac, bool run) {
+                                                     int64_t mode, int64_t pad, bool ac, std::array<bool, 2> mask, bool run) {
   const char* what = "grid_sample backward";
   check_modes(mode, pad, what);
   check_sample(input, grid, what);
   TORCH_CHECK(gout.dim() == 4 && gout.size(0) == input.size(0) && gout.size(1) == input.size(1) &&
                   gout.size(2) == grid.size(1) && gout.size(3) == grid.size(2),
               what, ": grad_out ", gout.sizes(), " must be (B, C, Ho, Wo)");
-  if (!run) return {at::empty(input.sizes(), input.options().dtype(at::kFloat)), at::empty(grid.sizes(), grid.options().dtype(at::kFloat))};
+  const auto xopt = input.options().dtype(at::kFloat), gopt = grid.options().dtype(at::kFloat);
+  if (!run)
+    return {at::empty(mask[0] ? input.sizes() : at::IntArrayRef{0}, xopt), at::empty(mask[1] ? grid.sizes() : at::IntArrayRef{0}, gopt)};
   Tensor go = gpu_f32(gout, "grad_out", what), x = gpu_f32(input, "input", what), gr = gpu_f32(grid, "grid", what);
-  Tensor gx = at::zeros_like(x), gg = at::empty_like(gr);
+  Tensor gx = mask[0] ? at::zeros_like(x) : at::empty({0}, xopt), gg = mask[1] ? at::empty_like(gr) : at::empty({0}, gopt);
   if (go.numel() == 0) return {gx, gg.zero_()};
+  if (!mask[0] && !mask[1]) return {gx, gg};
   c10::hip::HIPGuardMasqueradingAsCUDA g(x.device());
   check_status(oflow_grid_sample_backward_f32(go.data_ptr<float>(), x.data_ptr<float>(), gr.data_ptr<float>(), (int)x.size(0),
                                               (int)x.size(1), (int)x.size(2), (int)x.size(3), (int)gr.size(1), (int)gr.size(2),
-                                              (int)mode, (int)pad, ac ? 1 : 0, gx.data_ptr<float>(), gg.data_ptr<float>(),
-                                              cur_stream()),
+                                              (int)mode, (int)pad, ac ? 1 : 0, mask[0] ? gx.data_ptr<float>() : nullptr,
+                                              mask[1] ? gg.data_ptr<float>() : nullptr, cur_stream()),
                what);
   return {gx, gg};
 }
-std::tuple<Tensor, Tensor> grid_sample_backward_hip(const Tensor& go, const Tensor& x, const Tensor& gr, int64_t m, int64_t p, bool ac) {
-  return grid_sample_backward_impl(go, x, gr, m, p, ac, true);
+std::tuple<Tensor, Tensor> grid_sample_backward_hip(const Tensor& go, const Tensor& x, const Tensor& gr, int64_t m, int64_t p, bool ac,
+                                                    std::array<bool, 2> mask) {
+  return grid_sample_backward_impl(go, x, gr, m, p, ac, mask, true);
 }
-std::tuple<Tensor, Tensor> grid_sample_backward_meta(const Tensor& go, const Tensor& x, const Tensor& gr, int64_t m, int64_t p, bool ac) {
-  return grid_sample_backward_impl(go, x, gr, m, p, ac, false);
+std::tuple<Tensor, Tensor> grid_sample_backward_meta(const Tensor& go, const Tensor& x, const Tensor& gr, int64_t m, int64_t p, bool ac,
+                                                     std::array<bool, 2> mask) {
+  return grid_sample_backward_impl(go, x, gr, m, p, ac, mask, false);
 }
 
 // ---------------------------------------------------------------- backward (training path, §8(f) row 3)
@@ -490,7 +504,8 @@ std::vector<Tensor> lookup_backward_meta(const Tensor& go, const Tensor& co, int
 }
 
 // grads[0] += every coarser level's gradient pushed back through the floor 2x2 pools (native kernel), then
-// grad_f1 = f2 . G^T / sqrt(C), grad_f2 = f1 . G / sqrt(C) as batched GEMMs (hipBLASLt / rocBLAS via at::bmm)
+// grad_f1 = f2 . G^T / sqrt(C), grad_f2 = f1 . G / sqrt(C) as batched GEMMs on the fp32 matrix cores
+// (oflow_corr_fmap_grad_f32, csrc/corr_backward.hip)
 std::tuple<Tensor, Tensor> pyramid_backward_impl(const std::vector<Tensor>& level_grads, const Tensor& fmap1,
                                                  const Tensor& fmap2, bool run) {
   const char* what = "corr_pyramid_backward";
@@ -548,8 +563,8 @@ TORCH_LIBRARY(oflow, m) {
   m.def("grid_sample(Tensor input, Tensor grid, int mode, int padding_mode, bool align_corners) -> Tensor");
   m.def("corr_lookup_backward(Tensor grad_out, Tensor coords, int radius, int H, int W, int num_levels) -> Tensor[]");
   m.def("corr_pyramid_backward(Tensor[] level_grads, Tensor fmap1, Tensor fmap2) -> (Tensor, Tensor)");
-  m.def("grid_warp_backward(Tensor grad_out, Tensor frame, Tensor flow, int mode, int padding_mode, bool align_corners) -> (Tensor, Tensor)");
-  m.def("grid_sample_backward(Tensor grad_out, Tensor input, Tensor grid, int mode, int padding_mode, bool align_corners) -> (Tensor, Tensor)");
+  m.def("grid_warp_backward(Tensor grad_out, Tensor frame, Tensor flow, int mode, int padding_mode, bool align_corners, bool[2] output_mask) -> (Tensor, Tensor)");
+  m.def("grid_sample_backward(Tensor grad_out, Tensor input, Tensor grid, int mode, int padding_mode, bool align_corners, bool[2] output_mask) -> (Tensor, Tensor)");
 }
 
 TORCH_LIBRARY_IMPL(oflow, CUDA, m) {

@@ -91,11 +91,15 @@ __device__ __forceinline__ bool inb(int x, int y, int W, int H) {
   return static_cast<unsigned>(x) < static_cast<unsigned>(W) && static_cast<unsigned>(y) < static_cast<unsigned>(H);
 }
 
-// padding of one integer tap coordinate for bicubic (ATen compute_coordinates on a tap): returns the in-range index
-// or -1 (zeros padding, outside)
-__device__ __forceinline__ int tap_index(int i, int n, int pad, int ac) {
-  if (pad == OFLOW_PAD_ZEROS) return (static_cast<unsigned>(i) < static_cast<unsigned>(n)) ? i : -1;
-  float x = static_cast<float>(i);
+// padding of one bicubic tap coordinate, given as the float ATen forms (ix_nw - 1 + k; add_value_bounded /
+// get_value_bounded pad the float, then cast): returns the in-range index or -1 (zeros padding, outside). Far-out
+// coordinates (|x| >= 2^20) still land on the border / reflected pixel under border and reflection padding, as in the
+// forward (grid_warp.hip)
+__device__ __forceinline__ int tap_index(float x, int n, int pad, int ac) {
+  if (pad == OFLOW_PAD_ZEROS) {
+    const int i = to_index(x);
+    return (static_cast<unsigned>(i) < static_cast<unsigned>(n)) ? i : -1;
+  }
   if (pad == OFLOW_PAD_REFLECTION) {
     if (ac) {
       if (n <= 1) return 0;
@@ -227,12 +231,11 @@ __global__ __launch_bounds__(256) void warp_backward_kernel(WarpBwdArgs a) {
       cubic_coeffs(ty, cy);
       cubic_coeffs_grad(tx, dx);
       cubic_coeffs_grad(ty, dy);
-      const int x0 = to_index(fx) - 1, y0 = to_index(fy) - 1;
       int xi[4], yi[4];
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
-        xi[k] = (x0 == -1048577) ? -1 : tap_index(x0 + k, a.W, a.pad, a.ac);
-        yi[k] = (y0 == -1048577) ? -1 : tap_index(y0 + k, a.H, a.pad, a.ac);
+        xi[k] = tap_index(fx - 1.0f + static_cast<float>(k), a.W, a.pad, a.ac);
+        yi[k] = tap_index(fy - 1.0f + static_cast<float>(k), a.H, a.pad, a.ac);
       }
       for (int c = 0; c < a.C; ++c) {
         const float g = go[(size_t)c * HWo];

@@ -59,4 +59,8 @@ class GraphedRAFT:
         self.image0.copy_(image0, non_blocking=True)
         self.image1.copy_(image1, non_blocking=True)
         self.graph.replay()
+        if getattr(self.model, "range_guard", "off") == "sync":  # (the captured forward cannot read the flag)
+            from optical_flow import _native
+
+            _native.range_flag_raise_if_set(self.image0.device, "GraphedRAFT")
         return self.flow_low, self.flow_up

@@ -5,8 +5,8 @@ in eval mode), so the only communication is at the edges of the batch (SURVEY.md
   * ``scatter_pairs``: rank ``src`` holds the global (B, 3, H, W) pair batch and scatters contiguous shards,
     one per rank (RCCL lowers scatter to per-peer sends: each peer receives over its own xGMI link);
   * ``gather_flows``:  shards' flows go back to rank ``dst``.
-There is no per-iteration exchange, and with the global shape passed in (fixed per run) a step issues only the
-scatter and the two gathers: no metadata broadcast, no host sync. Ragged batches (B % world_size != 0) are padded
+There is no per-iteration exchange, and with the global shape passed in (fixed per run; checked against the source
+batch once, collectively) a step issues only the scatter and the two gathers: no metadata broadcast, no host sync. Ragged batches (B % world_size != 0) are padded
 to equal chunks for the collective and trimmed on both sides; a rank with no pair skips the forward. The same code runs on gloo with CPU tensors (tests).
 """
 from __future__ import annotations
@@ -42,23 +42,37 @@ def _meta(t: Optional[Tensor], src: int, group, device: torch.device) -> Sequenc
     return v[1 : 1 + v[0]]
 
 
-def scatter_pairs(
-    image0: Optional[Tensor],
-    image1: Optional[Tensor],
-    device: torch.device,
-    src: int = 0,
-    group=None,
-    shape: Optional[Sequence[int]] = None,
-) -> Tuple[Tensor, Tensor]:
-    """Scatter the pair batch held by rank ``src`` (other ranks pass ``None``); returns this rank's shard.
-    ``shape`` = the global (B, C, H, W) when every rank knows it (fixed per run: no metadata collective, no host
-    sync); otherwise it is broadcast from ``src``."""
+_VALIDATED = set()  # (shape, group, src) checked collectively once per process (see scatter_pairs)
+
+
+def _check_shape_collectively(shape, image0, image1, src: int, group, device: torch.device) -> None:
+    """Once per (shape, group, src) per process: rank ``src`` broadcasts whether its batch matches the caller-given
+    global ``shape`` and every rank raises the same ValueError on a mismatch (one 8-byte broadcast + one host sync
+    per run, not per step)."""
     world, rank = _world(group)
-    if shape is not None and rank == src:
-        # host-only check (no collective, no sync): a wrong ``shape`` would mis-size the scatter silently
-        for img in (image0, image1):
-            if tuple(img.shape) != tuple(shape):
-                raise ValueError(f"scatter_pairs: shape {tuple(shape)} does not match the source batch {tuple(img.shape)}")
+    key = (tuple(int(v) for v in shape), id(group) if group is not None else None, src)
+    if key in _VALIDATED:
+        return
+    ok = torch.zeros(1, dtype=torch.int64, device=device)
+    if rank == src:
+        ok[0] = int(all(tuple(img.shape) == tuple(shape) for img in (image0, image1)))
+    dist.broadcast(ok, src=dist.get_global_rank(group, src) if group is not None else src, group=group)
+    if not int(ok.item()):
+        got = tuple(image0.shape) if rank == src else "(held by the source rank)"
+        raise ValueError(f"scatter_pairs: shape {tuple(shape)} does not match the source batch {got}")
+    _VALIDATED.add(key)
+
+
+def _scatter(image0, image1, device, src, group, shape):
+    """The scatter; returns (shard0, shard1, error). A source batch that disagrees with a caller-given ``shape`` after
+    the one-time collective check (the source's batch changed shape mid-run) still completes the collective with
+    NaN pieces of the agreed size, so no peer blocks; the source gets the ValueError back to raise afterwards."""
+    world, rank = _world(group)
+    err = None
+    if shape is not None:
+        _check_shape_collectively(shape, image0, image1, src, group, device)
+        if rank == src and any(tuple(img.shape) != tuple(shape) for img in (image0, image1)):
+            err = ValueError(f"scatter_pairs: shape {tuple(shape)} does not match the source batch {tuple(image0.shape)}")
     shape = list(shape) if shape is not None else _meta(image0, src, group, device)
     b, rest = shape[0], shape[1:]
     chunk = -(-b // world)
@@ -68,17 +82,39 @@ def scatter_pairs(
         recv = torch.empty([chunk] + rest, dtype=torch.float32, device=device)
         scatter_list = None
         if rank == src:
-            img = img.to(device=device, dtype=torch.float32)
             scatter_list = []
-            for r in range(world):
-                s0, s1 = shard_bounds(b, world, r)
-                piece = img[s0:s1]
-                if s1 - s0 < chunk:
-                    piece = torch.cat([piece, piece.new_zeros([chunk - (s1 - s0)] + rest)], dim=0)
-                scatter_list.append(piece.contiguous())
+            if err is not None:  # poison: the agreed sizes, NaN values
+                scatter_list = [torch.full([chunk] + rest, float("nan"), device=device) for _ in range(world)]
+            else:
+                img = img.to(device=device, dtype=torch.float32)
+                for r in range(world):
+                    s0, s1 = shard_bounds(b, world, r)
+                    piece = img[s0:s1]
+                    if s1 - s0 < chunk:
+                        piece = torch.cat([piece, piece.new_zeros([chunk - (s1 - s0)] + rest)], dim=0)
+                    scatter_list.append(piece.contiguous())
         dist.scatter(recv, scatter_list, src=dist.get_global_rank(group, src) if group is not None else src, group=group)
         outs.append(recv[: stop - start])
-    return outs[0], outs[1]
+    return outs[0], outs[1], err
+
+
+def scatter_pairs(
+    image0: Optional[Tensor],
+    image1: Optional[Tensor],
+    device: torch.device,
+    src: int = 0,
+    group=None,
+    shape: Optional[Sequence[int]] = None,
+) -> Tuple[Tensor, Tensor]:
+    """Scatter the pair batch held by rank ``src`` (other ranks pass ``None``); returns this rank's shard.
+    ``shape`` = the global (B, C, H, W) when every rank knows it (fixed per run: after a one-time collective check that
+    it matches the source batch -- a mismatch raises ValueError on every rank -- a step issues no metadata collective
+    and no host sync); otherwise it is broadcast from ``src``. Should the source batch later stop matching ``shape``,
+    the source raises ValueError after completing the collective with NaN pieces (peers receive NaN, never block)."""
+    s0, s1, err = _scatter(image0, image1, device, src, group, shape)
+    if err is not None:
+        raise err
+    return s0, s1
 
 
 def gather_flows(flow: Tensor, global_batch: int, dst: int = 0, group=None) -> Optional[Tensor]:
@@ -117,13 +153,13 @@ def infer_sharded(
     sync (bench.py passes it; shapes are fixed per run). A rank whose shard is empty (B < world size) does not run
     ``forward``; it sends zero padding of ``flow_shapes`` = ((C, h, w) of flow_low, (C, H, W) of flow_up) -- without
     them it runs ``forward`` on one zero pair to learn the shapes and discards the result."""
-    s0, s1 = scatter_pairs(image0, image1, device, src=src, group=group, shape=shape)
+    s0, s1, err = _scatter(image0, image1, device, src, group, shape)
     b = int(shape[0]) if shape is not None else None
     if b is None:
         gb = torch.tensor([image0.shape[0] if dist.get_rank(group) == src else 0], dtype=torch.int64, device=device)
         dist.broadcast(gb, src=dist.get_global_rank(group, src) if group is not None else src, group=group)
         b = int(gb.item())
-    if s0.shape[0] == 0:
+    if s0.shape[0] == 0 or err is not None:  # no pair here, or a poisoned step on the source: pad the gathers
         if flow_shapes is None:
             z = s0.new_zeros([1] + list(s0.shape[1:]))
             lo, up = forward(z, z)
@@ -132,4 +168,7 @@ def infer_sharded(
         up = s0.new_zeros([0] + list(flow_shapes[1]))
     else:
         low, up = forward(s0, s1)
-    return gather_flows(low, b, dst=src, group=group), gather_flows(up, b, dst=src, group=group)
+    out = gather_flows(low, b, dst=src, group=group), gather_flows(up, b, dst=src, group=group)
+    if err is not None:  # every rank has completed the step's collectives
+        raise err
+    return out

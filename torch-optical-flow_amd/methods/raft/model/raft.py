@@ -112,6 +112,11 @@ class RAFT(nn.Module):
         # split encoders: the stem convolution builds its 7x7 patch operand from the image tile by tile
         # (OFLOW_IN_IMG7S2) instead of reading a patch matrix written beforehand (fnet's image0 rows shared with cnet)
         self.stem_from_image = True
+        # the split-fp16 range guard (csrc: a sticky device flag set when an operand's hi half overflows fp16): "sync"
+        # reads it at the end of every GPU inference forward (one 4-byte copy) and raises there; "deferred" reads it
+        # without waiting -- at a later forward once the GPU is past this one, or in check_range(); "off" never reads
+        self.range_guard = "sync"
+        self._range_pending = None
         # the split paths cache packed fp16 hi/lo weights keyed by (storage, version); parameters created under
         # torch.inference_mode() have no version counter, so loading new weights in place drops the caches
         for m in (self.fnet, self.cnet, self.update_block):
@@ -221,6 +226,18 @@ class RAFT(nn.Module):
             main.wait_stream(st)
         return outs
 
+    def check_range(self, device=None) -> None:
+        """Raise if a split-fp16 operand overflowed in any forward since the last check (waits for the GPU)."""
+        pend, self._range_pending = self._range_pending, None
+        if pend is not None:
+            pend[1].synchronize()
+            if int(pend[0].item()):
+                _native.range_flag(pend[2]).zero_()
+                raise RuntimeError("RAFT forward: a split-fp16 operand exceeded the fp16 range (|x| >= 65520) in an "
+                                   "earlier forward; its output is not valid")
+        if device is not None:
+            _native.range_flag_raise_if_set(device)
+
     def forward(
         self,
         image0: Tensor,
@@ -232,7 +249,29 @@ class RAFT(nn.Module):
     ) -> Union[Tensor, Tuple[Tensor, Tensor], List[Tensor]]:
         """Estimate optical flow between pairs of frames (`raft.py:87-147`). Images (B, 3, H, W) in [0, 255]
         with H, W divisible by 8 (use ``InputPadder``). Returns ``(coords1 - coords0, flow_up)`` in test mode,
-        else the list of ``iters`` upsampled predictions."""
+        else the list of ``iters`` upsampled predictions. On the GPU in inference, raises RuntimeError when a
+        split-fp16 operand left the fp16 range (``range_guard``)."""
+        guard = self.range_guard in ("sync", "deferred") and image0.is_cuda and not torch.is_grad_enabled()
+        capturing = image0.is_cuda and torch.cuda.is_current_stream_capturing()
+        if guard and not capturing:
+            _native.range_flag(image0.device)  # registered before the first kernel that may set it
+            pend = self._range_pending
+            if self.range_guard == "deferred" and pend is not None and pend[1].query():
+                self.check_range()
+        out = self._forward(image0, image1, iters, flow_init, test_mode)
+        if guard and not capturing:
+            dev = image0.device
+            if self.range_guard == "sync":
+                _native.range_flag_raise_if_set(dev, "RAFT forward")
+            elif self._range_pending is None:
+                host = torch.empty(1, dtype=torch.int32, pin_memory=True)
+                host.copy_(_native.range_flag(dev), non_blocking=True)
+                ev = torch.cuda.Event()
+                ev.record(torch.cuda.current_stream(dev))
+                self._range_pending = (host, ev, dev)
+        return out
+
+    def _forward(self, image0: Tensor, image1: Tensor, iters: int, flow_init: Optional[Tensor], test_mode: bool):
         image0 = (2 * (image0 / 255.0) - 1.0).contiguous()
         image1 = (2 * (image1 / 255.0) - 1.0).contiguous()
         hdim, cdim = self.hparams.hidden_dim, self.hparams.context_dim

@@ -71,10 +71,27 @@ SYMBOLS = (
     "oflow_corr_fmap_grad_f32",
     "oflow_grid_warp_backward_f32",
     "oflow_grid_sample_backward_f32",
+    "oflow_set_range_flag",
 )
 
 _lib = None
 _recorder = None  # optional {op name: [(start event, end event), ...]} filled around each launch
+_flops = None  # optional {"exec_f16": .., "useful": .., "fma_f32": ..} accumulated per launch (bench's step roofline)
+
+
+def set_flop_counter(counter):
+    """Accumulate, per matrix-core launch, the f16 MFMA flops the kernels issue (3 split products; channel padding to
+    32-channel groups and output-channel blocks included, pixel-tile padding not) under "exec_f16", the fp32-equivalent
+    flops of the layer's real channels under "useful", and the fp32 FMA flops of the small-grid flow head under
+    "fma_f32". ``counter``: a dict, or None to stop."""
+    global _flops
+    _flops = counter
+
+
+def _count(exec_f16: int, useful: int, fma: int = 0) -> None:
+    _flops["exec_f16"] = _flops.get("exec_f16", 0) + exec_f16
+    _flops["useful"] = _flops.get("useful", 0) + useful
+    _flops["fma_f32"] = _flops.get("fma_f32", 0) + fma
 
 
 def set_event_recorder(recorder):
@@ -201,6 +218,8 @@ def load() -> ctypes.CDLL:
     lib.oflow_flow2rgb_f32.argtypes = [P, I, I, I, I, I, F, F, I, I, F, P, P, P]
     lib.oflow_flow_pack_f32.restype = I
     lib.oflow_flow_pack_f32.argtypes = [P, I, I, I, I, I, P, P]
+    lib.oflow_set_range_flag.restype = I
+    lib.oflow_set_range_flag.argtypes = [P]
     v = lib.oflow_abi_version()
     if v != ABI_VERSION:
         raise RuntimeError(f"liboflow_hip.so ABI version {v}, expected {ABI_VERSION}: rebuild the library")
@@ -257,10 +276,13 @@ def _gpu_f32(t: torch.Tensor, name: str, what: str) -> torch.Tensor:
             f"{what}: {name} is on {t.device}; this MI355X build runs only on ROCm GPU tensors (no CPU fallback)"
         )
     if t.requires_grad and torch.is_grad_enabled():
-        # the kernels have no backward: fail loudly instead of returning a graph-less tensor
+        # these raw entry points (tiled / NHWC / split-fp16 / on-the-fly layouts, the inference kernels) have no
+        # autograd formula: fail loudly instead of returning a graph-less tensor. The differentiable path is the
+        # canonical one (CorrBlock under autograd, optical_flow.warp / grid_sample: native backward kernels)
         raise RuntimeError(
-            f"{what}: {name} requires grad; this build implements the inference path only (no backward kernels): "
-            "run under torch.no_grad() / torch.inference_mode(), or detach the input"
+            f"{what}: {name} requires grad; this entry point is an inference layout with no autograd formula: use "
+            "CorrBlock / optical_flow.warp (native backward kernels), or run under torch.no_grad() / "
+            "torch.inference_mode(), or detach the input"
         )
     if t.dtype != torch.float32:
         t = t.float()
@@ -342,6 +364,8 @@ def corr_pyramid_tiled_s32(f1: torch.Tensor, f2: torch.Tensor, num_levels: int =
         levels.append(store[off * q : (off + n) * q].view(q, n))
         off += n
     ptrs = (ctypes.c_void_p * MAX_LEVELS)(*[t.data_ptr() for t in levels])
+    if _flops is not None:  # the level-0 GEMM (pooling is the epilogue's)
+        _count(3 * 2 * b * (h * w) ** 2 * g * 32, 2 * b * (h * w) ** 2 * g * 32)
     with torch.cuda.device(f1.device), _Timed(what, f1.device):
         _check(lib.oflow_corr_pyramid_tiled_s32(f1.data_ptr(), f2.data_ptr(), b, g * 32, h, w, int(num_levels), ptrs,
                                                 _stream(f1.device)), what)
@@ -486,6 +510,38 @@ def corr_lookup_otf(f1h: torch.Tensor, f2h: Sequence[torch.Tensor], coords: torc
 
 
 ACT = {"none": 0, "relu": 1, "sigmoid": 2, "tanh": 3}
+
+# Range guard of the split-fp16 operands (always on): every kernel that writes or stages S32 values sets a sticky
+# device flag when a value's hi half would overflow fp16 (|x| >= 65520 or inf; include/oflow.h oflow_set_range_flag).
+# The RAFT forward reads it once (RAFT.range_guard) and raises; no per-convolution reduction or sync.
+_range_flags = {}
+
+
+def range_flag(device: torch.device) -> torch.Tensor:
+    """The device's range flag (one int32, registered with the library on first use for that device)."""
+    device = torch.device(device)
+    idx = device.index if device.index is not None else torch.cuda.current_device()
+    flag = _range_flags.get(idx)
+    if flag is None:
+        flag = torch.zeros(1, dtype=torch.int32, device=torch.device("cuda", idx))
+        with torch.cuda.device(idx):
+            torch.cuda.synchronize(idx)  # the zero fill is complete before any kernel may set it
+            _check(load().oflow_set_range_flag(ctypes.c_void_p(flag.data_ptr())), "set_range_flag")
+        _range_flags[idx] = flag
+    return flag
+
+
+def range_flag_raise_if_set(device: torch.device, what: str = "RAFT forward") -> None:
+    """Read the device's range flag (one D2H copy of 4 bytes: a sync of the current stream) and raise if a split-fp16
+    operand overflowed since the last check; the flag is cleared before raising."""
+    flag = range_flag(device)
+    if int(flag.item()):
+        flag.zero_()
+        raise RuntimeError(
+            f"{what}: a split-fp16 operand exceeded the fp16 range (|x| >= 65520) -- an activation outside the range "
+            "these kernels represent exactly; the output is not valid (OFLOW_CHECK=1 names the convolution)"
+        )
+
 
 # OFLOW_CHECK=1: before every split-fp16 convolution, a device-side max-abs reduction over its input (the values that
 # become fp16 hi + lo operands) raises if any |x| > 65504, where the hi half would overflow to inf. Debug mode: one
@@ -734,7 +790,7 @@ class ConvWeights:
     """A conv layer's weights packed for oflow_conv_s32: [in_groups][taps][n_pad][hi | lo] fp16 (per-output-channel
     power-of-two scaled so that max |w| = 2^14 keeps the lo halves normal), the inverse scales and the bias."""
 
-    __slots__ = ("pack", "wscale", "bias", "n", "n_pad", "kh", "kw", "kg", "layout")
+    __slots__ = ("pack", "wscale", "bias", "n", "n_pad", "kh", "kw", "kg", "layout", "cin")
 
     def __init__(self, weight: torch.Tensor, bias, n_pad: int, patches: bool = False):
         w = weight.detach().float()
@@ -761,6 +817,7 @@ class ConvWeights:
         self.wscale = inv
         self.bias = None if bias is None else bias.detach().float().contiguous()
         self.n, self.n_pad, self.kh, self.kw, self.kg = n, n_pad, kh, kw, kg
+        self.cin = c  # real input channels (flop accounting)
         self.layout = "conv"  # "convc1_frag": convc1_level_weights (the fused lookup + convc1's fragment-major order)
 
 
@@ -781,6 +838,7 @@ def convc1_level_weights(conv: torch.nn.Conv2d, num_levels: int, radius: int) ->
     frag = cw.pack.reshape(lg, 4, 2, 32, 2, 2, 2, 8)  # group, wave, ntile, r, hi/lo, sub, hh, 8
     cw.pack = frag.permute(0, 1, 2, 5, 4, 6, 3, 7).contiguous()
     cw.layout = "convc1_frag"
+    cw.cin = num_levels * kk
     return cw
 
 
@@ -803,6 +861,8 @@ def corr_lookup_convc1(pyr: "TiledPyramid", coords: torch.Tensor, radius: int, c
     ptrs = (ctypes.c_void_p * MAX_LEVELS)(*[t.data_ptr() for t in pyr.levels])
     hs = (ctypes.c_int * MAX_LEVELS)(*[d[0] for d in pyr.dims])
     ws = (ctypes.c_int * MAX_LEVELS)(*[d[1] for d in pyr.dims])
+    if _flops is not None:
+        _count(3 * 2 * b * h * w * 256 * cw.kg * 32, 2 * b * h * w * 256 * cw.cin)
     with torch.cuda.device(co.device), _Timed(what, co.device):
         _check(
             load().oflow_corr_lookup_convc1_s32(
@@ -868,6 +928,10 @@ def conv_s32(x: S32Slice, cw: ConvWeights, block_n: int, act: str = "none", out_
             raise RuntimeError(f"{what}: addend must be a GRU-epilogue fp32 [P, >= {cw.n}] view with 16-B aligned rows")
         ap, aps = addend.data_ptr(), addend.stride(0)
     dev = x.device
+    if _flops is not None:
+        taps, p_out = cw.kh * cw.kw, b * h * w  # (s2d only changes where the epilogue writes)
+        n_exec = -(-cw.n_pad // int(block_n)) * int(block_n)
+        _count(3 * 2 * p_out * n_exec * cw.kg * 32 * taps, 2 * p_out * cw.n * cw.cin * taps)
     with torch.cuda.device(dev), _Timed(f"conv{cw.kh}x{cw.kw}", dev):
         _check(
             load().oflow_conv_s32_ex3(
@@ -898,6 +962,9 @@ def flow_head2(x: "S32Slice", weight: torch.Tensor, bias: torch.Tensor, coords: 
         raise RuntimeError(f"{what}: bias must be fp32 (2,)")
     if coords.dtype != torch.float32 or not coords.is_contiguous() or tuple(coords.shape) != (b, 2, h, w):
         raise RuntimeError(f"{what}: coords must be contiguous fp32 ({b}, 2, {h}, {w})")
+    if _flops is not None:
+        fl = 2 * b * h * w * 2 * x.ng * 32 * 9
+        _count(0, fl, fl)
     with torch.cuda.device(coords.device), _Timed("conv3x3", coords.device):
         _check(load().oflow_flow_head2_s32(x.ptr, x.ps, x.ng, weight.data_ptr(), bias.data_ptr(), b, h, w,
                                            coords.data_ptr(), _stream(coords.device)), what)

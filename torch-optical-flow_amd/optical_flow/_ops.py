@@ -112,9 +112,11 @@ def _warp_backward(ctx, grad_out):
     frame, flow = ctx.saved_tensors
     mode, pad, ac = ctx.args
     # the native transpose (warp_backward.hip): grid = linspace base + flow, so the flow gradient is the grid gradient
-    g_in, g_flow = torch.ops.oflow.grid_warp_backward(grad_out.contiguous(), frame, flow, mode, pad, ac)
-    g_frame = g_in.to(frame.dtype) if ctx.needs_input_grad[0] else None
-    g_flow = g_flow.to(flow.dtype) if ctx.needs_input_grad[1] else None
+    # only the wanted outputs are formed (no zero fill / atomics for a frame that needs no gradient)
+    need = [bool(ctx.needs_input_grad[0]), bool(ctx.needs_input_grad[1])]
+    g_in, g_flow = torch.ops.oflow.grid_warp_backward(grad_out.contiguous(), frame, flow, mode, pad, ac, need)
+    g_frame = g_in.to(frame.dtype) if need[0] else None
+    g_flow = g_flow.to(flow.dtype) if need[1] else None
     return g_frame, g_flow, None, None, None
 
 
@@ -127,9 +129,10 @@ def _sample_setup(ctx, inputs, output):
 def _sample_backward(ctx, grad_out):
     inp, grid = ctx.saved_tensors
     mode, pad, ac = ctx.args
-    g_in, g_grid = torch.ops.oflow.grid_sample_backward(grad_out.contiguous(), inp, grid, mode, pad, ac)
-    g_x = g_in.to(inp.dtype) if ctx.needs_input_grad[0] else None
-    g_g = g_grid.to(grid.dtype) if ctx.needs_input_grad[1] else None
+    need = [bool(ctx.needs_input_grad[0]), bool(ctx.needs_input_grad[1])]
+    g_in, g_grid = torch.ops.oflow.grid_sample_backward(grad_out.contiguous(), inp, grid, mode, pad, ac, need)
+    g_x = g_in.to(inp.dtype) if need[0] else None
+    g_g = g_grid.to(grid.dtype) if need[1] else None
     return g_x, g_g, None, None, None
 
 
