@@ -362,6 +362,8 @@ def main() -> int:
                     help="replay each rank's forward from a HIP graph (model/graph.py: one launch per step)")
     ap.add_argument("--no-conv-benchmark", action="store_true",
                     help="disable torch.backends.cudnn.benchmark (MIOpen exhaustive find of the conv algorithms)")
+    ap.add_argument("--no-step-flops", action="store_true",
+                    help="skip the untimed flop-counting forward (roofline.step), e.g. under a kernel-trace profiler")
     ap.add_argument("--range-guard", default=None, choices=["sync", "deferred", "off"],
                     help="RAFT.range_guard (default: the model's, 'sync'); 'deferred' checks once after the timed region")
     args = ap.parse_args()
@@ -476,7 +478,7 @@ def main() -> int:
             epe = step_epe(out, gtag, gfix, global_batch)
         # one more (untimed) forward with the per-launch flop counter: the step roofline
         step_flops = None
-        if args.workload != "corr" and not args.graph:
+        if args.workload != "corr" and not args.graph and not args.no_step_flops:
             cnt = {}
             _native.set_flop_counter(cnt)
             fwd(img0[:ppg] if img0 is not None else torch.zeros((ppg, 3, h, w), device=dev),

@@ -15,5 +15,5 @@ tools/gpu_job.sh \
  "200|r4s1_bench_hd|python -u bench.py --workload hd" \
  "400|r4s1_pmcm|bash tools/pmc_mfma_job.sh" \
  "60|r4s1_pmcm_sum|python3 tools/pmc_mfma.py \$(find gpurun_out/pmcm/p1 -name '*counter_collection.csv' | head -1) \$(find gpurun_out/pmcm/p2 -name '*counter_collection.csv' | head -1) --json gpurun_out/r4s1_pmc_mfma.json; find gpurun_out/pmcm -name '*.csv' -size +20M -delete" \
- "300|r4s1_prof|rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/r4s1_prof -o run -- python3 bench.py --steps 6 --warmup 3 --no-cpu-baseline" \
+ "300|r4s1_prof|rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/r4s1_prof -o run -- python3 bench.py --steps 6 --warmup 3 --no-cpu-baseline --no-step-flops" \
  "60|r4s1_phases|T=\$(find gpurun_out/r4s1_prof -name '*kernel_trace.csv' | head -1); python3 tools/step_phases.py \$T --steps 4 && python3 tools/prof_summary.py \$T --steps 6 --skip-last 2 > gpurun_out/r4s1_breakdown.txt; cp \$(find gpurun_out/r4s1_prof -name '*kernel_stats.csv' | head -1) gpurun_out/r4s1_kernel_stats.csv; rm -f \$T"
