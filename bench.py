@@ -365,7 +365,7 @@ def main() -> int:
     ap.add_argument("--no-step-flops", action="store_true",
                     help="skip the untimed flop-counting forward (roofline.step), e.g. under a kernel-trace profiler")
     ap.add_argument("--range-guard", default=None, choices=["sync", "deferred", "off"],
-                    help="RAFT.range_guard (default: the model's, 'sync'); 'deferred' checks once after the timed region")
+                    help="RAFT.range_guard (default: the model's, 'deferred': checked after the timed region)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -473,7 +473,7 @@ def main() -> int:
         elapsed = time.perf_counter() - t0
         _native.set_event_recorder(None)
         if getattr(model, "range_guard", "off") == "deferred":
-            model.check_range(dev)  # every timed forward's split operands were in range
+            model.check_range(dev)  # every timed forward's split operands were in range (raises otherwise)
         if rank == 0 and gtag:
             epe = step_epe(out, gtag, gfix, global_batch)
         # one more (untimed) forward with the per-launch flop counter: the step roofline

@@ -359,6 +359,7 @@ def test_range_guard_raises_on_split_overflow(where):
     with torch.inference_mode():
         ref = model(p0, p1, iters=4, test_mode=True)
     bad = _model(RAFT)
+    bad.range_guard = "sync"
     a0, a1 = p0, p1
     if where == "images":
         a0, a1 = p0 * 1e6, p1 * 1e6
@@ -375,13 +376,27 @@ def test_range_guard_raises_on_split_overflow(where):
 
 
 def test_range_guard_deferred_mode():
-    """range_guard = "deferred": the forward does not wait for the flag; check_range() (or a later forward that finds
-    the GPU past the earlier one) raises."""
+    """range_guard = "deferred" (the default): the forward does not wait for the flag; check_range() raises, and so
+    does a later forward once the GPU has finished the overflowing one; GraphedRAFT replays are guarded the same way."""
+    from model.graph import GraphedRAFT
+
     img0, img1 = synthetic.synthetic_pair(1, 128, 160, seed=6)
+    p0, p1 = img0.to(DEV), img1.to(DEV)
     bad = _model(RAFT)
-    bad.range_guard = "deferred"
+    assert bad.range_guard == "deferred"
     with torch.inference_mode():
-        bad(img0.to(DEV) * 1e6, img1.to(DEV) * 1e6, iters=2, test_mode=True)
+        bad(p0 * 1e6, p1 * 1e6, iters=2, test_mode=True)
         with pytest.raises(RuntimeError, match="fp16 range"):
             bad.check_range()
         bad.check_range()  # cleared
+        bad(p0 * 1e6, p1 * 1e6, iters=2, test_mode=True)
+        torch.cuda.synchronize()
+        with pytest.raises(RuntimeError, match="fp16 range"):
+            bad(p0, p1, iters=2, test_mode=True)  # reports the earlier forward
+        bad.check_range(DEV)
+        g = GraphedRAFT(bad, p0, p1, iters=2)
+        g(p0, p1)
+        bad.check_range(DEV)
+        g(p0 * 1e6, p1 * 1e6)
+        with pytest.raises(RuntimeError, match="fp16 range"):
+            bad.check_range(DEV)

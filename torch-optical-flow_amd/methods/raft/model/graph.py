@@ -58,9 +58,10 @@ class GraphedRAFT:
             )
         self.image0.copy_(image0, non_blocking=True)
         self.image1.copy_(image1, non_blocking=True)
+        guard = getattr(self.model, "range_guard", "off") in ("sync", "deferred")
+        if guard:  # (the captured forward cannot read the range flag: the model's guard runs around the replay)
+            self.model._range_before(self.image0.device)
         self.graph.replay()
-        if getattr(self.model, "range_guard", "off") == "sync":  # (the captured forward cannot read the flag)
-            from optical_flow import _native
-
-            _native.range_flag_raise_if_set(self.image0.device, "GraphedRAFT")
+        if guard:
+            self.model._range_after(self.image0.device)
         return self.flow_low, self.flow_up

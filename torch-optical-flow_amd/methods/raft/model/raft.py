@@ -112,10 +112,12 @@ class RAFT(nn.Module):
         # split encoders: the stem convolution builds its 7x7 patch operand from the image tile by tile
         # (OFLOW_IN_IMG7S2) instead of reading a patch matrix written beforehand (fnet's image0 rows shared with cnet)
         self.stem_from_image = True
-        # the split-fp16 range guard (csrc: a sticky device flag set when an operand's hi half overflows fp16): "sync"
-        # reads it at the end of every GPU inference forward (one 4-byte copy) and raises there; "deferred" reads it
-        # without waiting -- at a later forward once the GPU is past this one, or in check_range(); "off" never reads
-        self.range_guard = "sync"
+        # the split-fp16 range guard (csrc: a sticky device flag set when an operand's hi half overflows fp16).
+        # "deferred" (default): each GPU inference forward snapshots the flag asynchronously (pinned copy + event); a
+        # later forward raises once the GPU is past the overflowing one, and check_range() waits and raises -- no
+        # host sync in the forward. "sync": read at the end of every forward and raise there (one 4-byte D2H copy, a
+        # host sync per forward: -2.5 % on the 8-pair bench step, profiles/r04/s1_bench*.log). "off": never read.
+        self.range_guard = "deferred"
         self._range_pending = None
         # the split paths cache packed fp16 hi/lo weights keyed by (storage, version); parameters created under
         # torch.inference_mode() have no version counter, so loading new weights in place drops the caches
@@ -254,22 +256,32 @@ class RAFT(nn.Module):
         guard = self.range_guard in ("sync", "deferred") and image0.is_cuda and not torch.is_grad_enabled()
         capturing = image0.is_cuda and torch.cuda.is_current_stream_capturing()
         if guard and not capturing:
-            _native.range_flag(image0.device)  # registered before the first kernel that may set it
-            pend = self._range_pending
-            if self.range_guard == "deferred" and pend is not None and pend[1].query():
-                self.check_range()
+            self._range_before(image0.device)
         out = self._forward(image0, image1, iters, flow_init, test_mode)
         if guard and not capturing:
-            dev = image0.device
-            if self.range_guard == "sync":
-                _native.range_flag_raise_if_set(dev, "RAFT forward")
-            elif self._range_pending is None:
-                host = torch.empty(1, dtype=torch.int32, pin_memory=True)
-                host.copy_(_native.range_flag(dev), non_blocking=True)
-                ev = torch.cuda.Event()
-                ev.record(torch.cuda.current_stream(dev))
-                self._range_pending = (host, ev, dev)
+            self._range_after(image0.device)
         return out
+
+    def _range_before(self, dev) -> None:
+        """Register the device's range flag; in deferred mode raise for an earlier forward the GPU has finished."""
+        _native.range_flag(dev)  # registered before the first kernel that may set it
+        pend = self._range_pending
+        if self.range_guard == "deferred" and pend is not None and pend[1].query():
+            self.check_range()
+
+    def _range_after(self, dev) -> None:
+        """After a forward's kernels are enqueued: read the flag now ("sync") or snapshot it ("deferred")."""
+        if self.range_guard == "sync":
+            _native.range_flag_raise_if_set(dev, "RAFT forward")
+        elif self.range_guard == "deferred":
+            pend = self._range_pending
+            if pend is None:
+                pend = (torch.empty(1, dtype=torch.int32, pin_memory=True), torch.cuda.Event(), dev)
+            elif not pend[1].query():
+                return  # the pending snapshot is still in flight; the flag is sticky, the next one will see this forward
+            pend[0].copy_(_native.range_flag(dev), non_blocking=True)
+            pend[1].record(torch.cuda.current_stream(dev))
+            self._range_pending = pend
 
     def _forward(self, image0: Tensor, image1: Tensor, iters: int, flow_init: Optional[Tensor], test_mode: bool):
         image0 = (2 * (image0 / 255.0) - 1.0).contiguous()

@@ -150,6 +150,8 @@ def main(
         for slot in slots:
             if slot is not None:
                 slot["future"].result()
+        model.check_range(device)  # the split-fp16 range guard of the last pairs' forwards (earlier ones: checked as
+        # the loop went on, RAFT.range_guard "deferred")
     return count
 
 
