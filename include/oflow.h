@@ -195,6 +195,12 @@ int oflow_flow_prep_s32(const float* d_coords, int B, int H, int W, void* d_patc
  * coords (B, 2, H, W) fp32 in place (raft.py:133 `coords1 = coords1 + delta_flow`), from an S32 input of in_groups
  * groups (1..8): fp32 FMAs on the exact S32 values; d_weight (2, C, 3, 3) fp32 as the nn.Conv2d stores it, d_bias [2].
  * Built for small grids (one image at 1/8 resolution); larger ones run faster as oflow_conv_s32 with n_pad 32. */
+/* oflow_flow_head_col2im_f32: d_coords (B, 2, H, W) += d_bias[c] + sum_{ky,kx} d_y[b][(ky*3+kx)*2 + c][y+ky-1][x+kx-1]
+ * (zero outside the image): the flow head's output conv (update.py:35-36, conv2 3x3 C -> 2, raft.py:133 coords1 +=
+ * delta_flow) as a 1x1 conv C -> 18 per-tap products (oflow_conv_s32 with an fp32 NCHW destination d_y (B, 18, H, W))
+ * followed by this gather. */
+int oflow_flow_head_col2im_f32(const float* d_y, const float* d_bias, int B, int H, int W, float* d_coords, void* stream);
+
 /* oflow_set_range_flag: register d_flag (one unsigned int in device memory of the current device; NULL: off) as the
  * range flag of the split-fp16 operands. Every kernel that writes or stages S32 values (the conv epilogues and staging,
  * norm_apply, pack / flow_prep, the fused lookup + convc1) sets it to 1 (atomic or) when a value's hi half overflows

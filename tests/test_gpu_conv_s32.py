@@ -410,3 +410,33 @@ def test_instance_norm_partials(kh, c, n, bn, h, w, tiles8):
     ea = float(((alpha.double() - a_ref).abs() / a_ref).max())
     eb = float(((beta.double() - b_ref).abs() / (mean.abs() * a_ref + 1.0)).max())
     assert ea <= 2e-6 and eb <= 2e-6, (ea, eb)
+
+
+@pytest.mark.parametrize("b,h,w", [(4, 55, 128), (2, 13, 45), (1, 1, 1), (3, 47, 156)])
+def test_flow_head_col2im_matches_fp64_and_conv(b, h, w):
+    """The flow head's output conv (update.py:36, 3x3 256 -> 2, bias; raft.py:133 coords1 += delta) as a 1x1 conv
+    256 -> 18 (per-tap products) + oflow_flow_head_col2im_f32, against float64 F.conv2d of the same split operands, and
+    against the 3x3 conv_s32 path (fp32 reordering apart): borders (zero padding), a 1x1 grid, KITTI's 47x156."""
+    from model.update import SplitUpdate  # noqa: F401  (the weight layout under test is SplitUpdate's "fh2T")
+
+    g = torch.Generator().manual_seed(b * 1000 + h + w)
+    x = torch.relu(torch.randn(b, 256, h, w, generator=g) * 2.0).to(DEV)
+    wt = (torch.randn(2, 256, 3, 3, generator=g) / math.sqrt(256 * 9)).to(DEV)
+    bias = torch.randn(2, generator=g).to(DEV)
+    coords = (torch.randn(b, 2, h, w, generator=g) * 30.0).to(DEV)
+    xs = N.s32_from_f32(x)
+    xe = N.s32_to_f32(xs, 256)  # the exact operand values the kernels see (hi + lo)
+    ref, bound = _ref(xe, wt, bias, 3, 3)
+    ref = ref + coords.double()
+    cw_t = N.ConvWeights(wt.permute(2, 3, 0, 1).reshape(18, 256, 1, 1), None, 32)
+    y = torch.empty(b, 18, h, w, device=DEV)
+    c1 = coords.clone()
+    with torch.inference_mode():
+        N.conv_s32(N.S32Slice(xs), cw_t, 32, f32=y)
+        N.flow_head_col2im(y, bias, c1)
+        c2 = coords.clone()
+        N.conv_s32(N.S32Slice(xs), N.ConvWeights(wt, bias, 32), 32, f32=c2, f32_accumulate=True)
+    tol = 2e-6 * bound + 1e-6 + 2e-7 * coords.double().abs()
+    assert bool(((c1.double() - ref).abs() <= tol).all()), float((c1.double() - ref).abs().max())
+    assert bool(((c2.double() - ref).abs() <= tol).all())
+    assert float((c1 - c2).abs().max()) <= 1e-4

@@ -94,6 +94,11 @@ struct ConvArgs {
 constexpr int kInS32 = OFLOW_IN_S32, kInF32Norm = OFLOW_IN_F32_NORM, kInF32 = OFLOW_IN_F32, kInImg = OFLOW_IN_IMG7S2;
 // kInImg: the stem's 7x7/2 pad-3 window of a 3-channel image, staged per tile (TY = 4 rows x 32 columns)
 constexpr int kImgC = 3, kImgK = 7, kImgRows = (kTY - 1) * 2 + kImgK, kImgCols = (kTX - 1) * 2 + kImgK;
+// the window in LDS: [c][row][column parity][column / 2] (row pitch kImgPitch floats): output column x reads window
+// column 2x + kx at (kx & 1) * kImgHalf + x + (kx >> 1), so the 32 lanes of one output row read 32 consecutive floats
+// (conflict-free ds_read_b32; the column-interleaved [c][row][col] image gave each 32-lane group 2- to 4-way conflicts:
+// 50 % of the stem's LDS cycles, profiles/r04/s1_pmc_mfma.json)
+constexpr int kImgHalf = (kImgCols + 1) / 2, kImgPitch = 2 * kImgHalf, kImgPlane = kImgRows * kImgPitch;
 
 __device__ __forceinline__ float act_fn(float v, int act) {
   if (act == 1) return v < 0.f ? 0.f : v;  // relu; NaN propagates like ATen
@@ -177,7 +182,7 @@ __global__ __launch_bounds__(64 * WM * WN, WM * WN == 8 ? 1 : 2) void conv_s32_k
   constexpr int EPI_BYTES = BM * TS * 4;
   constexpr int LDS_BYTES = MAIN_BYTES > EPI_BYTES ? MAIN_BYTES : EPI_BYTES;
   // kInImg: the stem's input window [c][row][col] + one zero float, then the patch channels' window offsets
-  constexpr int kImgZero = kImgC * kImgRows * kImgCols;
+  constexpr int kImgZero = kImgC * kImgPlane;
   constexpr int IMG_FLOATS = (kImgZero + 1 + 3) & ~3;
   constexpr int AFF_BYTES = AIN == kInF32Norm ? kAinGroups * 32 * 8  // float2 (scale, shift) per input channel
                             : AIN == kInImg ? IMG_FLOATS * 4 + 160 * 4
@@ -190,7 +195,7 @@ __global__ __launch_bounds__(64 * WM * WN, WM * WN == 8 ? 1 : 2) void conv_s32_k
   // instance-norm partials per (row of waves, channel): (count, mean, M2)
   __shared__ float3 sStat[EPI == 0 ? WM * BN : 1];
   float2* sAff = reinterpret_cast<float2*>(smem + LDS_BYTES);
-  float* sImg = reinterpret_cast<float*>(smem + LDS_BYTES);  // kInImg: [c][row][col], zero at kImgZero
+  float* sImg = reinterpret_cast<float*>(smem + LDS_BYTES);  // kInImg: [c][row][parity][col/2], zero at kImgZero
   int* sKoff = reinterpret_cast<int*>(smem + LDS_BYTES + (AIN == kInImg ? IMG_FLOATS * 4 : 0));
   uint8_t* sA = smem;
   uint8_t* sB = smem + (ADB ? 2 : 1) * A_BYTES;
@@ -256,7 +261,9 @@ __global__ __launch_bounds__(64 * WM * WN, WM * WN == 8 ? 1 : 2) void conv_s32_k
 #define OFLOW_WRITE_A(RA, BUF, G)                                                                                    \
   if (!OFLOW_ABL(4)) _Pragma("unroll") for (int s_ = 0; s_ < APER; ++s_) {                                           \
     const int item = tid + s_ * NTH;                                                                            \
-    const int p = item >> 3, c = item & 7;                                                                           \
+    /* image input: consecutive lanes take consecutive pixels of one chunk (conflict-free window reads); else the   \
+       8 chunks of a pixel (whole 128-B LDS rows per 8 lanes) */                                                     \
+    const int p = AIN == kInImg ? item % BM : item >> 3, c = AIN == kInImg ? item / BM : item & 7;                   \
     if (AITEMS % NTH == 0 || item < AITEMS) {                                                                   \
       if constexpr (AIN != kInS32) {                                                                                 \
         /* 4 fp32 channels (G*32 + 4c ..) [-> relu(x * scale + shift)] -> 4 hi + 4 lo halves (8 B each) */           \
@@ -264,7 +271,7 @@ __global__ __launch_bounds__(64 * WM * WN, WM * WN == 8 ? 1 : 2) void conv_s32_k
         half4_ h4 = {0, 0, 0, 0}, l4 = {0, 0, 0, 0};                                                                 \
         if constexpr (AIN == kInImg) {                                                                               \
           /* patch channel k of pixel p = the staged window at (2*py, 2*px) + the channel's table offset */          \
-          const int pb_ = 2 * (p >> 5) * kImgCols + 2 * (p & 31);                                                    \
+          const int pb_ = 2 * (p >> 5) * kImgPitch + (p & 31);                                                       \
           const int4 ko_ = *reinterpret_cast<const int4*>(sKoff + (G) * 32 + 4 * c);                                 \
           const int kov_[4] = {ko_.x, ko_.y, ko_.z, ko_.w};                                                          \
           float mx_ = 0.f;                                                                                           \
@@ -381,10 +388,11 @@ __global__ __launch_bounds__(64 * WM * WN, WM * WN == 8 ? 1 : 2) void conv_s32_k
         float v = 0.f;
         if (static_cast<unsigned>(iy) < static_cast<unsigned>(2 * a.H) && static_cast<unsigned>(ix) < static_cast<unsigned>(2 * a.W))
           v = img[((long long)ch * (2 * a.H) + iy) * (2 * a.W) + ix];
-        sImg[e] = v;
+        sImg[ch * kImgPlane + ry * kImgPitch + (rx & 1) * kImgHalf + (rx >> 1)] = v;
       }
     } else {
     float iv[IMG_PER];
+    int io[IMG_PER];
 #pragma unroll
     for (int s_ = 0; s_ < IMG_PER; ++s_) {
       const int e = min(tid + s_ * NTH, IMG_N - 1);
@@ -395,15 +403,17 @@ __global__ __launch_bounds__(64 * WM * WN, WM * WN == 8 ? 1 : 2) void conv_s32_k
       const int cy = min(max(iy, 0), 2 * a.H - 1), cx = min(max(ix, 0), 2 * a.W - 1);
       const float v = img[((long long)ch * (2 * a.H) + cy) * (2 * a.W) + cx];
       iv[s_] = in ? v : 0.f;
+      io[s_] = ch * kImgPlane + ry * kImgPitch + (rx & 1) * kImgHalf + (rx >> 1);
     }
 #pragma unroll
     for (int s_ = 0; s_ < IMG_PER; ++s_)
-      if (tid + s_ * NTH < IMG_N) sImg[tid + s_ * NTH] = iv[s_];
+      if (tid + s_ * NTH < IMG_N) sImg[io[s_]] = iv[s_];
     }
     // patch channel k = t*3 + ch, t = ky*7 + kx -> window offset ch*(rows*cols) + ky*cols + kx (-1: zero, k >= 147)
     for (int k = tid; k < 160; k += NTH) {
       const int t = k / kImgC, ch = k - t * kImgC;
-      sKoff[k] = t < kImgK * kImgK ? (ch * kImgRows + t / kImgK) * kImgCols + t % kImgK : -1;
+      const int ky = t / kImgK, kx = t - ky * kImgK;
+      sKoff[k] = t < kImgK * kImgK ? ch * kImgPlane + ky * kImgPitch + (kx & 1) * kImgHalf + (kx >> 1) : -1;
     }
     if (tid == 0) sImg[kImgZero] = 0.f;
     __syncthreads();

@@ -207,6 +207,38 @@ __global__ __launch_bounds__(1024) void flow_head2_kernel(const uint8_t* __restr
   }
 }
 
+// coords (B, 2, H, W) += bias + sum over the 9 taps of the 3x3 conv's per-tap products y (B, 18, H, W) gathered at the
+// tap's neighbour (zero padding): the second half of the flow head's output conv (update.py:35-36 conv2, 3x3 C -> 2)
+// computed as a 1x1 conv C -> 18 (channel (ky*3+kx)*2 + c = the tap's contribution, evaluated at the INPUT pixel) and
+// this col2im. One thread per output pixel; the plane reads are coalesced along x.
+__global__ __launch_bounds__(256) void flow_head_col2im_kernel(const float* __restrict__ y, int B, int H, int W,
+                                                               const float* __restrict__ bias, float* __restrict__ coords) {
+  const int HW = H * W;
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= B * HW) return;
+  const int b = t / HW, p = t - b * HW, py = p / W, px = p - py * W;
+  const float* yb = y + (size_t)b * 18 * HW;
+  float s[2] = {0.f, 0.f};
+#pragma unroll
+  for (int ky = 0; ky < 3; ++ky) {
+    const int yy = py + ky - 1;
+#pragma unroll
+    for (int kx = 0; kx < 3; ++kx) {
+      const int xx = px + kx - 1;
+      const bool in = static_cast<unsigned>(yy) < static_cast<unsigned>(H) && static_cast<unsigned>(xx) < static_cast<unsigned>(W);
+      const int q = in ? yy * W + xx : p;
+#pragma unroll
+      for (int c = 0; c < 2; ++c) {
+        const float v = yb[(size_t)((ky * 3 + kx) * 2 + c) * HW + q];
+        s[c] += in ? v : 0.f;
+      }
+    }
+  }
+  float* cb = coords + (size_t)b * 2 * HW + p;
+  cb[0] += s[0] + bias[0];  // delta_flow = conv2(.) incl. its bias; coords1 = coords1 + delta_flow (raft.py:133)
+  cb[HW] += s[1] + bias[1];
+}
+
 }  // namespace
 OFLOW_RANGE_FLAG_SETTER(s32io)
 }  // namespace oflow
@@ -241,6 +273,16 @@ extern "C" int oflow_flow_prep_s32(const float* d_coords, int B, int H, int W, v
   hipLaunchKernelGGL(flow_prep_kernel, dim3((unsigned)((items + 255) / 256)), dim3(256), 0, static_cast<hipStream_t>(stream),
                      d_coords, B, H, W, static_cast<uint8_t*>(d_patches), static_cast<uint8_t*>(d_flow0),
                      flow0_pixel_stride, static_cast<uint8_t*>(d_flow1), flow1_pixel_stride);
+  return launch_status();
+}
+
+extern "C" int oflow_flow_head_col2im_f32(const float* d_y, const float* d_bias, int B, int H, int W, float* d_coords,
+                                          void* stream) {
+  if (!d_y || !d_bias || !d_coords) return OFLOW_E_NULL;
+  if (B <= 0 || H <= 0 || W <= 0 || (long long)B * H * W * 18 >= (1LL << 31)) return OFLOW_E_SHAPE;
+  const int P = B * H * W;
+  hipLaunchKernelGGL(flow_head_col2im_kernel, dim3((unsigned)((P + 255) / 256)), dim3(256), 0, static_cast<hipStream_t>(stream),
+                     d_y, B, H, W, d_bias, d_coords);
   return launch_status();
 }
 

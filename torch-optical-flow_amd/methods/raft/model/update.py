@@ -22,6 +22,10 @@ from optical_flow import _native
 
 # output-channel block (workgroup N) per update-block conv of the split path; tools/exp/run_conv_bn_ab.py A/Bs them
 CONV_BN = {"c2": 64, "f1": 128, "f2": 64, "mo": 128, "gru": 128, "fh1": 128}
+# the flow head's output conv (3x3, 256 -> 2) above the small-grid threshold: "col2im" = a 1x1 conv 256 -> 18 (the 9
+# taps' products at the input pixel, 18 of 32 MFMA columns used) + a gather of the 9 taps into coords1
+# (oflow_flow_head_col2im_f32); "conv" = the 3x3 conv with 2 of its 32 output columns used, coords1 += in its epilogue
+FLOW_HEAD_MODE = "col2im"
 
 class FlowHead(nn.Module):
     def __init__(self, input_dim: int = 128, hidden_dim: int = 256) -> None:
@@ -242,6 +246,8 @@ class SplitUpdate:
         self.pm = S(b, h, w, 4, dev)
         self.f1 = S(b, h, w, 4, dev)
         self.fh = S(b, h, w, 8, dev)
+        self.fh2y = None  # (B, 18, H, W) per-tap products of the flow head's output conv (flow_head_mode "col2im")
+        self.flow_head_mode = getattr(block, "flow_head_mode", FLOW_HEAD_MODE)
         self.hm = torch.empty((b * h * w, hdim), device=dev, dtype=torch.float32)
         self.z = torch.empty_like(self.hm)
         V = _native.S32Slice
@@ -276,6 +282,10 @@ class SplitUpdate:
             "mo": CW(enc.conv.weight, enc.conv.bias, 128),
             "fh1": CW(fh.conv1.weight, fh.conv1.bias, 256),
             "fh2": CW(fh.conv2.weight, fh.conv2.bias, 32),
+            # the output conv as a 1x1 conv C -> 18 (channel (ky*3+kx)*2 + c: tap (ky, kx)'s share of output c, taken at
+            # the input pixel) + oflow_flow_head_col2im_f32, which gathers the 9 taps and adds the bias into coords1
+            "fh2T": CW(fh.conv2.weight.detach().float().permute(2, 3, 0, 1).reshape(18, -1, 1, 1), None, 32),
+            "fh2_bias": fh.conv2.bias.detach().float().contiguous(),
             # small grids: the 2-channel output conv as fp32 FMAs (oflow_flow_head2_s32) on the conv's own weights
             "fh2_f32": (fh.conv2.weight.detach().float().contiguous(), fh.conv2.bias.detach().float().contiguous()),
             "m1": CW(block.mask[0].weight, block.mask[0].bias, 256),
@@ -363,6 +373,11 @@ class SplitUpdate:
         conv(net, w["fh1"], CONV_BN["fh1"], "relu", y0=V(self.fh))
         if self.flow_head_fma and coords1.is_contiguous():
             _native.flow_head2(V(self.fh), *w["fh2_f32"], coords1)  # coords1 += conv2(.) (raft.py:133)
+        elif self.flow_head_mode == "col2im" and coords1.is_contiguous():
+            if self.fh2y is None:
+                self.fh2y = torch.empty((b, 18, h, wd), device=coords1.device, dtype=torch.float32)
+            conv(V(self.fh), w["fh2T"], 32, f32=self.fh2y)
+            _native.flow_head_col2im(self.fh2y, w["fh2_bias"], coords1)  # coords1 += conv2(.) (raft.py:133)
         else:
             conv(V(self.fh), w["fh2"], 32, f32=coords1, f32_accumulate=True)
         if not need_mask:

@@ -72,6 +72,7 @@ SYMBOLS = (
     "oflow_grid_warp_backward_f32",
     "oflow_grid_sample_backward_f32",
     "oflow_set_range_flag",
+    "oflow_flow_head_col2im_f32",
 )
 
 _lib = None
@@ -220,6 +221,8 @@ def load() -> ctypes.CDLL:
     lib.oflow_flow_pack_f32.argtypes = [P, I, I, I, I, I, P, P]
     lib.oflow_set_range_flag.restype = I
     lib.oflow_set_range_flag.argtypes = [P]
+    lib.oflow_flow_head_col2im_f32.restype = I
+    lib.oflow_flow_head_col2im_f32.argtypes = [P, P, I, I, I, P, P]
     v = lib.oflow_abi_version()
     if v != ABI_VERSION:
         raise RuntimeError(f"liboflow_hip.so ABI version {v}, expected {ABI_VERSION}: rebuild the library")
@@ -968,6 +971,22 @@ def flow_head2(x: "S32Slice", weight: torch.Tensor, bias: torch.Tensor, coords: 
     with torch.cuda.device(coords.device), _Timed("conv3x3", coords.device):
         _check(load().oflow_flow_head2_s32(x.ptr, x.ps, x.ng, weight.data_ptr(), bias.data_ptr(), b, h, w,
                                            coords.data_ptr(), _stream(coords.device)), what)
+
+
+def flow_head_col2im(y: torch.Tensor, bias: torch.Tensor, coords: torch.Tensor) -> None:
+    """coords += bias + the 3x3 gather of the per-tap products y (B, 18, H, W) (oflow_flow_head_col2im_f32): the flow
+    head's output conv as 1x1 conv C -> 18 + col2im (update.py:36, raft.py:133)."""
+    what = "flow_head_col2im"
+    b, _, h, w = coords.shape
+    if coords.dtype != torch.float32 or not coords.is_contiguous() or coords.shape[1] != 2 or coords.device.type != "cuda":
+        raise RuntimeError(f"{what}: coords must be contiguous fp32 (B, 2, H, W) on the GPU")
+    if y.dtype != torch.float32 or not y.is_contiguous() or tuple(y.shape) != (b, 18, h, w) or y.device != coords.device:
+        raise RuntimeError(f"{what}: y must be contiguous fp32 ({b}, 18, {h}, {w})")
+    if bias is None or bias.dtype != torch.float32 or tuple(bias.shape) != (2,) or bias.device != coords.device:
+        raise RuntimeError(f"{what}: bias must be fp32 (2,) on the coords' device")
+    with torch.cuda.device(coords.device), _Timed("flow_head_col2im", coords.device):
+        _check(load().oflow_flow_head_col2im_f32(y.data_ptr(), bias.data_ptr(), b, h, w, coords.data_ptr(),
+                                                 _stream(coords.device)), what)
 
 
 def stem_patches(img: torch.Tensor, out: torch.Tensor) -> torch.Tensor:
