@@ -22,10 +22,12 @@ from optical_flow import _native
 
 # output-channel block (workgroup N) per update-block conv of the split path; tools/exp/run_conv_bn_ab.py A/Bs them
 CONV_BN = {"c2": 64, "f1": 128, "f2": 64, "mo": 128, "gru": 128, "fh1": 128}
-# the flow head's output conv (3x3, 256 -> 2) above the small-grid threshold: "col2im" = a 1x1 conv 256 -> 18 (the 9
-# taps' products at the input pixel, 18 of 32 MFMA columns used) + a gather of the 9 taps into coords1
-# (oflow_flow_head_col2im_f32); "conv" = the 3x3 conv with 2 of its 32 output columns used, coords1 += in its epilogue
-FLOW_HEAD_MODE = "col2im"
+# the flow head's output conv (3x3, 256 -> 2) above the small-grid threshold: "conv" = the 3x3 conv with 2 of its 32
+# output columns used, coords1 += in its epilogue; "col2im" = a 1x1 conv 256 -> 18 (the 9 taps' products at the input
+# pixel, 18 of 32 MFMA columns used) + a gather of the 9 taps into coords1 (oflow_flow_head_col2im_f32). In-process A/B
+# of the 8-pair step: col2im 19.99 / 19.85 ms (median / min) vs conv 19.93 / 19.74 (profiles/r04/s2_ab_fh.log): in the
+# step the other pair lane fills the CUs the 2-column conv leaves idle, so "conv" stays the default
+FLOW_HEAD_MODE = "conv"
 
 class FlowHead(nn.Module):
     def __init__(self, input_dim: int = 128, hidden_dim: int = 256) -> None:
