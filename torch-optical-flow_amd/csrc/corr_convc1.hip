@@ -96,7 +96,7 @@ __global__ __launch_bounds__(kNT, 2) void corr_convc1_kernel(C1Args a) {
   __shared__ __attribute__((aligned(16))) uint8_t smem[LDS_BYTES];
   __shared__ float2 sSB[kN];
   __shared__ float2 sC[kQM];
-  __shared__ int4 sO[NS][kQM];    // window origin x0, y0, -, dx = x0 & 3
+  __shared__ int4 sO[NS][kQM];    // window origin x0, y0, masks (x: bits 0-15, y: bits 16-31), dx
   __shared__ float4 sW[NS][kQM];  // bilinear weights (nw, ne, sw, se)
   uint8_t* sA = smem;
   float* sP = reinterpret_cast<float*>(smem + A_BYTES);
@@ -130,9 +130,12 @@ __global__ __launch_bounds__(kNT, 2) void corr_convc1_kernel(C1Args a) {
     int xs, ys;
     float4 w4;
     window_origin(cx, cy, __int_as_float((127 - l) << 23), R, xs, ys, w4);  // 1/2^l exactly (corr.py:68)
-    (void)Hl;
-    (void)Wl;
-    sO[l & (NS - 1)][qd] = make_int4(xs, ys, 0, xs & 3);  // (z unused: validity is decided per chunk at the gather)
+    const int dx = xs & 3, xa = xs - dx;
+    const int xl = max(0, -xa), xh = min(4 * NCH, Wl - xa);
+    const int yl = max(0, -ys), yh = min(PK, Hl - ys);
+    const unsigned xm = xh > xl ? (((1u << (xh - xl)) - 1u) << xl) : 0u;
+    const unsigned ym = yh > yl ? (((1u << (yh - yl)) - 1u) << yl) : 0u;
+    sO[l & (NS - 1)][qd] = make_int4(xs, ys, static_cast<int>(xm | (ym << 16)), dx);
     sW[l & (NS - 1)][qd] = w4;
   };
 
@@ -152,43 +155,49 @@ __global__ __launch_bounds__(kNT, 2) void corr_convc1_kernel(C1Args a) {
   // A's taps past KK (the last group's tail) are never written again: zero the whole A buffer once
   for (int e = tid; e < A_BYTES / 16; e += kNT) reinterpret_cast<u32x4*>(sA)[e] = u32x4{0u, 0u, 0u, 0u};
   __syncthreads();
-  // chunk items: lane = query (ql = tid & 63), item s of wave w = window chunk idx = 4s + w -> (row u, chunk k) =
-  // (idx / NCH, idx % NCH), wave-uniform. The query's window origin is read once per level, each item's offset is a
-  // few full-rate ops, and the patch writes of one instruction go to 64 queries at the odd pitch QS.
-  static_assert(CITEMS == kNT * NI && (PK * NCH) % 4 == 0, "four waves cover a query's window chunks exactly");
-  const int ql = tid & (kQM - 1), wv = __builtin_amdgcn_readfirstlane(tid >> 6);
-  auto chunk_of = [&](int s, int& u, int& k) {
-    const int idx = 4 * s + wv;  // wave-uniform
-    u = idx / NCH;
-    k = idx - u * NCH;
+  // chunk item s of this thread -> (query, window row, chunk): recomputed per use (a few full-rate ops; no live
+  // registers across the level)
+  static_assert(magic16_ok(PK * NCH, CITEMS) && magic16_ok(NCH, PK * NCH), "chunk item decode");
+  auto item_of = [&](int s, int& q, int& u, int& k) {
+    int t_ = tid;
+    asm volatile("" : "+v"(t_));
+    const unsigned item = static_cast<unsigned>(min(t_ + kNT * s, CITEMS - 1));
+    q = static_cast<int>(__umul24(item, magic16(PK * NCH)) >> 16);
+    const unsigned rm = item - static_cast<unsigned>(q) * (PK * NCH);
+    u = static_cast<int>(__umul24(rm, magic16(NCH)) >> 16);
+    k = static_cast<int>(rm - static_cast<unsigned>(u) * NCH);
   };
 
   u32x4 rv[NI];
-  unsigned rok = 0u;  // bit s: item s holds in-level cells (else its chunk is written as zeros)
   auto gather = [&](int l) {
     int Hl, Wl, WB, LF;
     const float* base;
     level(l, Hl, Wl, WB, LF, base);
     const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
         const_cast<float*>(base + (size_t)q0 * LF), (short)0, nq * LF * 4, 0x00020000);
-    const int4 o = sO[l & (NS - 1)][ql];
-    const int xa = o.x - o.w;
-    const int qoff = __umul24(ql, LF);
-    rok = 0u;
+    constexpr int HB = (NI + 1) / 2;  // two batches of window reads: fewer live registers
 #pragma unroll
-    for (int s = 0; s < NI; ++s) {
-      int u, k;
-      chunk_of(s, u, k);
-      const int y = o.y + u, xc = xa + 4 * k;
-      // needed: the row inside the level, the chunk's first column inside [0, W_l) (xa is a multiple of 4: a chunk
-      // lies wholly left of the level or starts inside it), and the chunk inside the window
-      const bool need = static_cast<unsigned>(y) < static_cast<unsigned>(Hl) &&
-                        static_cast<unsigned>(xc) < static_cast<unsigned>(Wl) && 4 * k < o.w + PK;
-      int off = (qoff + (__umul24(static_cast<unsigned>(y) >> 2, WB) + (xc >> 3)) * 32 + ((y & 3) << 3) + (xc & 7)) * 4;
-      asm volatile("" : "+v"(off));  // computed unconditionally: a select, not an exec branch around it
-      off = need ? off : 0;
-      rok |= (need ? 1u : 0u) << s;
-      rv[s] = __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0);
+    for (int s0 = 0; s0 < NI; s0 += HB) {
+      int4 o[NI];
+      int qs[NI], us[NI], ks[NI];
+#pragma unroll
+      for (int s = s0; s < (NI < s0 + HB ? NI : s0 + HB); ++s) {
+        item_of(s, qs[s], us[s], ks[s]);
+        o[s] = sO[l & (NS - 1)][qs[s]];
+      }
+#pragma unroll
+      for (int s = s0; s < (NI < s0 + HB ? NI : s0 + HB); ++s) {
+        const int q = qs[s], u = us[s], k = ks[s];
+        const int y = o[s].y + u, xc = (o[s].x - o[s].w) + 4 * k;
+        // the chunk holds a needed, in-level cell: row u valid, one of its 4 columns valid and inside the window
+        const unsigned need = ((static_cast<unsigned>(o[s].z) >> 16) >> u) & 1u &
+                              (((static_cast<unsigned>(o[s].z) & 0xffffu) >> (4 * k)) & 15u ? 1u : 0u) &
+                              (4 * k < o[s].w + PK ? 1u : 0u);
+        int off = (__umul24(q, LF) + (__umul24(static_cast<unsigned>(y) >> 2, WB) + (xc >> 3)) * 32 + ((y & 3) << 3) + (xc & 7)) * 4;
+        asm volatile("" : "+v"(off));  // computed unconditionally: a select, not an exec branch around it
+        off = need ? off : 0;
+        rv[s] = __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0);
+      }
     }
   };
   const __amdgpu_buffer_rsrc_t rsW =
@@ -217,21 +226,17 @@ __global__ __launch_bounds__(kNT, 2) void corr_convc1_kernel(C1Args a) {
   auto body = [&](int l, auto Pc) {
     constexpr int P = decltype(Pc)::value;
     // ---- 1. chunks -> LDS patches (cells outside the level zeroed) ----
-    {
-      int Hl, Wl, WB, LF;
-      const float* base;
-      level(l, Hl, Wl, WB, LF, base);
-      const int4 o = sO[l & (NS - 1)][ql];
-      const int lim = Wl - (o.x - o.w);  // cells of the window row from xa on that lie inside the level
 #pragma unroll
-      for (int s = 0; s < NI; ++s) {
-        int u, k;
-        chunk_of(s, u, k);
+    for (int s = 0; s < NI; ++s) {
+      if (CITEMS % kNT == 0 || tid + kNT * s < CITEMS) {
+        int q, u, k;
+        item_of(s, q, u, k);
+        const int4 o = sO[l & (NS - 1)][q];
+        const unsigned m = (((static_cast<unsigned>(o.z) >> 16) >> u) & 1u) ? ((static_cast<unsigned>(o.z) >> (4 * k)) & 15u) : 0u;
         const float* fv = reinterpret_cast<const float*>(&rv[s]);
-        const bool ok = (rok >> s) & 1u;
-        float* dst = sP + ql * QS + u * RW + 3 + 4 * k - o.w;
+        float* dst = sP + q * QS + u * RW + 3 + 4 * k - o.w;
 #pragma unroll
-        for (int e = 0; e < 4; ++e) dst[e] = (ok && 4 * k + e < lim) ? fv[e] : 0.0f;
+        for (int e = 0; e < 4; ++e) dst[e] = ((m >> e) & 1u) ? fv[e] : 0.0f;
       }
     }
     __syncthreads();  // patches complete; every wave is past level l-1's MFMAs (A free)
