@@ -362,6 +362,9 @@ def main() -> int:
                     help="replay each rank's forward from a HIP graph (model/graph.py: one launch per step)")
     ap.add_argument("--no-conv-benchmark", action="store_true",
                     help="disable torch.backends.cudnn.benchmark (MIOpen exhaustive find of the conv algorithms)")
+    ap.add_argument("--inflight", type=int, default=1,
+                    help="steps in flight: step i is issued on stream i %% N (its own side streams), so step i+1's "
+                         "encoders run beside step i's update loop (pairs are independent; every step's flows are its own)")
     ap.add_argument("--no-step-flops", action="store_true",
                     help="skip the untimed flop-counting forward (roofline.step), e.g. under a kernel-trace profiler")
     ap.add_argument("--range-guard", default=None, choices=["sync", "deferred", "off"],
@@ -454,9 +457,15 @@ def main() -> int:
             return infer_sharded(fwd, img0, img1, dev, shape=shard_shape, flow_shapes=flow_shapes)
         return fwd(img0, img1)
 
+    streams = [torch.cuda.current_stream(dev)] + [torch.cuda.Stream(device=dev) for _ in range(max(1, args.inflight) - 1)]
+
+    def issue(i):
+        with torch.cuda.stream(streams[i % len(streams)]):
+            return step()
+
     with torch.inference_mode():
-        for _ in range(args.warmup):
-            step()
+        for i in range(max(args.warmup, len(streams))):
+            issue(i)
         torch.cuda.synchronize(dev)
         # graph replays launch no Python, so no per-kernel events (the roofline comes from an eager run)
         rec = ({"*": True} if args.conv_events else {}) if not (args.no_events or args.graph) else None
@@ -465,8 +474,8 @@ def main() -> int:
             dist.barrier()
         torch.cuda.synchronize(dev)
         t0 = time.perf_counter()
-        for _ in range(args.steps):
-            out = step()
+        for i in range(args.steps):
+            out = issue(i)
         torch.cuda.synchronize(dev)
         if world > 1:
             dist.barrier()
@@ -535,6 +544,7 @@ def main() -> int:
             "conv_benchmark": not args.no_conv_benchmark,
             "update_impl": args.update_impl,
             "hip_graph": bool(args.graph),
+            "steps_in_flight": max(1, args.inflight),
         },
     }
     if rec and args.conv_events:

@@ -400,3 +400,27 @@ def test_range_guard_deferred_mode():
         g(p0 * 1e6, p1 * 1e6)
         with pytest.raises(RuntimeError, match="fp16 range"):
             bad.check_range(DEV)
+
+
+def test_forwards_in_flight_on_two_streams_equal_sequential():
+    """Pipelined steps (bench.py --inflight): forwards issued back to back from two streams -- each with its own side
+    and lane streams, the packed-weight caches shared behind an event -- give the flows of sequential forwards bit for
+    bit, including the very first forward on the second stream (weights packed by the first)."""
+    img0, img1 = synthetic.synthetic_pair(3, 128, 160, seed=8)
+    p0, p1 = img0.to(DEV), img1.to(DEV)
+    q0, q1 = torch.roll(p0, 5, dims=-1), torch.roll(p1, 5, dims=-1)
+    model = _model(RAFT)
+    with torch.inference_mode():
+        ref_a = model(p0, p1, iters=6, test_mode=True)
+        ref_b = model(q0, q1, iters=6, test_mode=True)
+        torch.cuda.synchronize()
+        fresh = _model(RAFT)  # empty caches: the second stream's first forward finds weights packed on the first
+        s = [torch.cuda.current_stream(), torch.cuda.Stream()]
+        outs = []
+        for i in range(4):
+            with torch.cuda.stream(s[i % 2]):
+                outs.append(fresh(*((p0, p1) if i % 2 == 0 else (q0, q1)), iters=6, test_mode=True))
+        torch.cuda.synchronize()
+    for i, (lo, up) in enumerate(outs):
+        ref = ref_a if i % 2 == 0 else ref_b
+        assert torch.equal(lo, ref[0]) and torch.equal(up, ref[1]), i

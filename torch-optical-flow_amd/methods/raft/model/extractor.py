@@ -149,13 +149,10 @@ class SplitEncoder:
             raise RuntimeError("SplitEncoder: batch norm needs eval mode (running statistics)")
         self.enc = enc
         self.inorm = enc.norm_fn == "instance"
-        from .update import tensor_key
+        from .update import cached_pack, tensor_key
 
         key = tuple(tensor_key(q) for q in enc.parameters()) + tuple(tensor_key(q) for q in enc.buffers())
-        cache = enc.__dict__.get("_split_weights")
-        if cache is None or cache[0] != key:
-            enc.__dict__["_split_weights"] = (key, self._pack(enc))
-        self.w = enc.__dict__["_split_weights"][1]
+        self.w = cached_pack(enc, key, lambda: self._pack(enc))
 
     def _cw(self, conv: nn.Conv2d, norm, **kw):
         if self.inorm or norm is None:

@@ -229,7 +229,8 @@ class RAFT(nn.Module):
         return outs
 
     def check_range(self, device=None) -> None:
-        """Raise if a split-fp16 operand overflowed in any forward since the last check (waits for the GPU)."""
+        """Raise if a split-fp16 operand overflowed in any forward since the last check (waits for the GPU; with
+        ``device`` for every stream of it)."""
         pend, self._range_pending = self._range_pending, None
         if pend is not None:
             pend[1].synchronize()
@@ -238,7 +239,7 @@ class RAFT(nn.Module):
                 raise RuntimeError("RAFT forward: a split-fp16 operand exceeded the fp16 range (|x| >= 65520) in an "
                                    "earlier forward; its output is not valid")
         if device is not None:
-            _native.range_flag_raise_if_set(device)
+            _native.range_flag_raise_if_set(device, all_streams=True)
 
     def forward(
         self,

@@ -184,11 +184,32 @@ _SIDE_STREAMS = {}
 
 
 def _side_stream(device: torch.device, slot: int = 0) -> "torch.cuda.Stream":
-    """A persistent extra stream per (device, slot), reused across forwards."""
-    key = (torch.device(device).index, slot)
+    """A persistent extra stream per (device, owner stream, slot), reused across forwards. The owner is the stream
+    current at the call: forwards issued from different streams (pipelined steps) get disjoint side streams."""
+    dev = torch.device(device)
+    owner = torch.cuda.current_stream(dev).stream_id
+    key = (dev.index, owner, slot)
     if key not in _SIDE_STREAMS:
         _SIDE_STREAMS[key] = torch.cuda.Stream(device=device)
     return _SIDE_STREAMS[key]
+
+
+def cached_pack(module: nn.Module, key, build):
+    """The packed weights cached on ``module`` for ``key`` (built by ``build()`` on a miss). The packing kernels run on
+    the stream current at the miss; an event recorded after them is waited on by every later user's current stream, so a
+    forward issued from another stream (pipelined steps) never reads weights still being written."""
+    cache = module.__dict__.get("_split_weights")
+    if cache is not None and cache[0] == key:
+        if cache[2] is not None:
+            torch.cuda.current_stream().wait_event(cache[2])
+        return cache[1]
+    w = build()
+    ev = None
+    if torch.cuda.is_available() and torch.cuda.is_initialized():
+        ev = torch.cuda.Event()
+        ev.record(torch.cuda.current_stream())
+    module.__dict__["_split_weights"] = (key, w, ev)
+    return w
 
 
 def tensor_key(q: Tensor):
@@ -270,10 +291,10 @@ class SplitUpdate:
 
     @staticmethod
     def _weights(block: BasicUpdateBlock):
-        key = _weights_key(block)
-        cache = block.__dict__.get("_split_weights")
-        if cache is not None and cache[0] == key:
-            return cache[1]
+        return cached_pack(block, _weights_key(block), lambda: SplitUpdate._pack(block))
+
+    @staticmethod
+    def _pack(block: BasicUpdateBlock):
         enc, gru, fh = block.encoder, block.gru, block.flow_head
         CW = _native.ConvWeights
         w = {
@@ -304,7 +325,6 @@ class SplitUpdate:
             w["q" + tag] = CW(hmf(cq.weight), None, 128)
             w["inp" + tag] = CW(torch.cat([cz.weight, cr.weight, cq.weight])[:, 128:256],
                                 torch.cat([cz.bias, cr.bias, cq.bias]), 384)
-        block.__dict__["_split_weights"] = (key, w)
         return w
 
     def step(self, corr_fn, coords1: Tensor, need_mask: bool, mask_out: Optional[Tensor] = None) -> Optional[Tensor]:

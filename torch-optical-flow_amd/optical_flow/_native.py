@@ -534,10 +534,13 @@ def range_flag(device: torch.device) -> torch.Tensor:
     return flag
 
 
-def range_flag_raise_if_set(device: torch.device, what: str = "RAFT forward") -> None:
-    """Read the device's range flag (one D2H copy of 4 bytes: a sync of the current stream) and raise if a split-fp16
-    operand overflowed since the last check; the flag is cleared before raising."""
+def range_flag_raise_if_set(device: torch.device, what: str = "RAFT forward", all_streams: bool = False) -> None:
+    """Read the device's range flag (one D2H copy of 4 bytes: a sync of the current stream, or of the whole device with
+    ``all_streams``: forwards in flight on other streams) and raise if a split-fp16 operand overflowed since the last
+    check; the flag is cleared before raising."""
     flag = range_flag(device)
+    if all_streams:
+        torch.cuda.synchronize(device)
     if int(flag.item()):
         flag.zero_()
         raise RuntimeError(
