@@ -119,3 +119,36 @@ def test_load_state_dict_drops_packed_weight_caches():
         m.__dict__["_split_weights"] = ("stale", {})
     model.invalidate_weight_caches()
     assert all("_split_weights" not in m.__dict__ for m in mods)
+
+
+def test_bench_batch_golden_and_step_epe(golden):
+    """bench.py's parity leg (host logic): the benchmarked workloads find their reference-generated batch golden, and
+    the EPE of the golden's own flows against itself is exactly 0 (per pair, strided full-res included)."""
+    import bench
+
+    for wl, tag in (("sintel", "sintel8"), ("kitti", "kitti8")):
+        _, h, w, iters, _, _ = bench.WORKLOADS[wl]
+        t, g = bench.batch_golden(wl, h, w, iters)
+        assert t == tag and g is not None
+        b, gh, gw, _, s, _ = (int(v) for v in g[f"{tag}_cfg"])
+        low = torch.from_numpy(g[f"{tag}_low"])
+        # a full-res flow whose stride-s samples are the golden's
+        up = torch.zeros(b, 2, gh, gw)
+        up[..., ::s, ::s] = torch.from_numpy(g[f"{tag}_up"])
+        e = bench.step_epe((low, up), t, g, 8)
+        assert e["pairs"] == 8 and e["low_max"] == 0.0 and e["up_max"] == 0.0
+    assert bench.batch_golden("sintel", 436, 1024, 24) == (None, None)  # other iteration counts: no batch golden
+    assert bench.batch_golden("hd", 1080, 1920, 12) == (None, None)
+
+
+def test_cached_pack_keys_and_rebuilds():
+    """The packed-weight cache (model.update.cached_pack): a hit returns the cached object, a new key rebuilds; on a
+    CPU-only host no event is recorded."""
+    from model.update import cached_pack
+
+    m = torch.nn.Linear(2, 2)
+    calls = []
+    a = cached_pack(m, ("k", 1), lambda: calls.append(1) or {"w": 1})
+    b = cached_pack(m, ("k", 1), lambda: calls.append(2) or {"w": 2})
+    c = cached_pack(m, ("k", 2), lambda: calls.append(3) or {"w": 3})
+    assert a is b and c == {"w": 3} and calls == [1, 3]
