@@ -48,7 +48,9 @@ class GraphedRAFT:
             torch.cuda.current_stream(dev).wait_stream(side)
             torch.cuda.synchronize(dev)
             self.graph = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(self.graph):
+            # captured on the warm-up stream: the side / lane streams the forward forks to (keyed by their owner
+            # stream, model/update.py _side_stream) are the ones the warm-up created
+            with torch.cuda.graph(self.graph, stream=side):
                 self.flow_low, self.flow_up = model(self.image0, self.image1, iters=iters, test_mode=True)
 
     def __call__(self, image0: Tensor, image1: Tensor) -> Tuple[Tensor, Tensor]:

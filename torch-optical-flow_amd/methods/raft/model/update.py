@@ -200,7 +200,9 @@ def cached_pack(module: nn.Module, key, build):
     forward issued from another stream (pipelined steps) never reads weights still being written."""
     cache = module.__dict__.get("_split_weights")
     if cache is not None and cache[0] == key:
-        if cache[2] is not None:
+        # (not while a graph is being captured: the capture must not depend on an event recorded outside it; a
+        # capture follows warm-up forwards and a device sync, so the weights are complete)
+        if cache[2] is not None and not torch.cuda.is_current_stream_capturing():
             torch.cuda.current_stream().wait_event(cache[2])
         return cache[1]
     w = build()
