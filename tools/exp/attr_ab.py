@@ -46,8 +46,12 @@ def main():
             elif attr.startswith("bn:"):  # an update-block conv's output-channel block (model.update.CONV_BN)
                 from model import update as U
                 U.CONV_BN[attr[3:]] = int(v)
-            else:
-                setattr(model, attr, v)
+            else:  # a model attribute, or a dotted path to a sub-module's attribute (update_block.split_streams)
+                obj = model
+                *path, name = attr.split(".")
+                for part in path:
+                    obj = getattr(obj, part)
+                setattr(obj, name, v)
 
     with torch.inference_mode():
         for k in arms:
