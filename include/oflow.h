@@ -291,6 +291,19 @@ int oflow_conv_s32_ex3(const void* d_x, long long x_pixel_stride, int in_groups,
                        long long res_pixel_stride, int res_activation, int s2d, int in_format,
                        const float* d_in_scale, const float* d_in_shift, const float* d_addend,
                        long long addend_pixel_stride, void* stream);
+/* oflow_conv_s32_ex4: oflow_conv_s32_ex3 plus d_wfrag, an optional fragment-major copy of d_wpack (same bytes, reordered
+ * [group][tap][n/32][slice][hi|lo][k half][row][8] so that one wave's 32x16 MFMA B fragment is 1 KB contiguous and is
+ * loaded straight into registers, skipping the LDS staging of B). Used for block_n 128 convolutions with more than one
+ * tap; other shapes ignore it. NULL = ex3. */
+int oflow_conv_s32_ex4(const void* d_x, long long x_pixel_stride, int in_groups, const void* d_wpack, int n_pad,
+                       const float* d_wscale, const float* d_bias, int N, int B, int H, int W, int kh, int kw,
+                       int block_n, int epilogue, int activation, float out_scale, void* d_y0, long long y0_pixel_stride,
+                       void* d_y1, long long y1_pixel_stride, float* d_f32, long long f32_batch_stride,
+                       long long f32_channel_stride, int f32_accumulate, float* d_gru_h, float* d_gru_z,
+                       int gru_channels, float* d_nhwc, int nhwc_pixel_stride, float* d_stats, const void* d_res,
+                       long long res_pixel_stride, int res_activation, int s2d, int in_format,
+                       const float* d_in_scale, const float* d_in_shift, const float* d_addend,
+                       long long addend_pixel_stride, const void* d_wfrag, void* stream);
 int oflow_stem_patches_s32(const float* d_img, int B, int C, int H, int W, void* d_out, int out_groups, void* stream);
 int oflow_norm_stats_finalize(const float* d_partials, int B, int tiles, int n_pad, int C, double eps, float* d_alpha,
                               float* d_beta, void* stream);

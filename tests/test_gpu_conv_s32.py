@@ -440,3 +440,49 @@ def test_flow_head_col2im_matches_fp64_and_conv(b, h, w):
     assert bool(((c1.double() - ref).abs() <= tol).all()), float((c1.double() - ref).abs().max())
     assert bool(((c2.double() - ref).abs() <= tol).all())
     assert float((c1 - c2).abs().max()) <= 1e-4
+
+
+@pytest.mark.parametrize("kh,kw,cin,epi,b,h,w", [
+    (3, 3, 256, 0, 2, 70, 130),   # even group count
+    (3, 3, 352, 0, 1, 131, 131),  # odd group count with odd taps: the two-group loop body's one-group tail
+    (3, 3, 32, 0, 4, 45, 97),     # one group
+    (1, 5, 384, 1, 2, 66, 130),   # GRU z|r gates (epilogue 1)
+    (5, 1, 384, 2, 2, 66, 130),   # GRU candidate (epilogue 2)
+    (5, 1, 96, 0, 3, 61, 100),    # odd group count, odd taps
+])
+def test_conv_register_weights_bit_identical(monkeypatch, kh, kw, cin, epi, b, h, w):
+    """The register-direct weight path (ConvWeights.frag -> oflow_conv_s32_ex4, BREG kernels; grids over 16384 output
+    pixels at block_n 128) against the LDS-staged one: the same MFMAs in the same order per output, so every output
+    bit-identical; plus the fp64 bound of test_conv_s32_matches_fp64 for the plain epilogue."""
+    g = torch.Generator().manual_seed(kh * 100 + cin + epi)
+    x = (torch.randn(b, cin, h, w, generator=g) * 1.5).to(DEV)
+    n = 256 if epi == 1 else 128
+    wt = (torch.randn(n, cin, kh, kw, generator=g) / math.sqrt(cin * kh * kw)).to(DEV)
+    bias = torch.randn(n, generator=g).to(DEV)
+    cw = N.ConvWeights(wt, bias, n)
+    xs = N.s32_from_f32(x)
+    ch = 128
+
+    def run(breg):
+        monkeypatch.setattr(N, "CONV_BREG", breg)
+        y = N.s32_empty(b, h, w, 4, DEV, zero=True)
+        if epi == 0:
+            f32 = torch.zeros(b, n, h, w, device=DEV)
+            N.conv_s32(N.S32Slice(xs), cw, 128, act="relu", y0=N.S32Slice(y), f32=f32)
+            torch.cuda.synchronize()
+            return f32, y, None, None
+        hm = torch.tanh(torch.randn(b * h * w, ch, generator=torch.Generator().manual_seed(1))).to(DEV)
+        z = torch.rand(b * h * w, ch, generator=torch.Generator().manual_seed(2)).to(DEV)
+        N.conv_s32(N.S32Slice(xs), cw, 128, epilogue=epi, y0=N.S32Slice(y), gru_h=hm, gru_z=z)
+        torch.cuda.synchronize()
+        return None, y, hm, z
+
+    a, c = run(True), run(False)
+    for u, v in zip(a, c):
+        if u is not None:
+            assert torch.equal(u, v)
+    if epi == 0:
+        ref, bound = _ref(N.s32_to_f32(xs, cin), wt, bias, kh, kw)
+        err = (a[0].double() - torch.relu(ref)).abs()
+        assert bool((err <= 2e-6 * bound + 1e-6).all()), float(err.max())
+

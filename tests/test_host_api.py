@@ -152,3 +152,18 @@ def test_cached_pack_keys_and_rebuilds():
     b = cached_pack(m, ("k", 1), lambda: calls.append(2) or {"w": 2})
     c = cached_pack(m, ("k", 2), lambda: calls.append(3) or {"w": 3})
     assert a is b and c == {"w": 3} and calls == [1, 3]
+
+
+def test_conv_frag_pack_is_a_permutation():
+    """ConvWeights.frag holds exactly the pack's halves, fragment-major: element (g, t, n, hl, k) of the pack at
+    [g][t][n / 32][k / 16][hl][(k / 8) % 2][n % 32][k % 8]."""
+    from optical_flow import _native as N
+
+    g = torch.Generator().manual_seed(5)
+    wt = torch.randn(96, 64, 3, 3, generator=g)
+    cw = N.ConvWeights(wt, None, 128)
+    f = cw.frag()
+    assert f is cw.frag() and f.shape == (2, 9, 4, 2, 2, 2, 32, 8)
+    p = cw.pack
+    for (gg, t, n, hl, k) in [(0, 0, 0, 0, 0), (1, 8, 127, 1, 31), (0, 4, 33, 1, 9), (1, 2, 95, 0, 17)]:
+        assert torch.equal(f[gg, t, n // 32, k // 16, hl, (k // 8) % 2, n % 32, k % 8], p[gg, t, n, hl, k])

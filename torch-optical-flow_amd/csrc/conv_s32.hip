@@ -88,6 +88,7 @@ struct ConvArgs {
   int ain;                 // input format: kInS32 / kInF32Norm / kInF32
   int cin;                 // kInF32: real input channels (row pitch cin * 4 B); channels >= cin stage as zeros
   int wbytes;              // bytes of the packed weights (kg * taps * npad * 128)
+  const uint8_t* wf;       // the same weights fragment-major (register-direct B, BREG kernels), or null
   int exp_flags;           // experiments only (oflow_exp_set_conv_flags): bit 0 = the stem's element-wise window loop
 };
 // input formats of oflow_conv_s32_ex2
@@ -158,7 +159,14 @@ __device__ __forceinline__ void store_s32(uint8_t* y, long long ps, long long P,
 //   6. read sub-step 0's operands of step i+1                            -> in flight during 7
 //   7. MFMAs of sub-step 1
 // so every LDS read has a block of MFMAs to hide behind, and the one barrier per step sits between two MFMA blocks.
-template <int KH, int KW, int BN, int WM, int WN, int EPI, int TY = kTY, int AIN = kInS32>
+//
+// BREG (register-direct weights, T > 1, 4 waves as 1 x 4: each wave all 128 pixels x one 32-channel tile): B comes from
+// the fragment-major copy of the weights (ConvArgs.wf: per step and channel tile [sub-step 2][hi, lo][lane 64][16 B],
+// one wave instruction = 1 KB contiguous = the MFMA's B fragment) straight into a 2-deep ring of operand registers --
+// no B staging through LDS, and the only barriers are the two around each input group's halo swap (T steps per group
+// instead of one barrier per step). No two waves load the same fragment. Same MFMAs in the same order per accumulator
+// as the LDS-staged kernel: bit-identical outputs.
+template <int KH, int KW, int BN, int WM, int WN, int EPI, int TY = kTY, int AIN = kInS32, bool BREG = false>
 __global__ __launch_bounds__(64 * WM * WN, WM * WN == 8 ? 1 : 2) void conv_s32_kernel(ConvArgs a) {
   constexpr int NTH = 64 * WM * WN;  // 4 waves (two workgroups per CU) or 8 (one)
   constexpr int T = KH * KW;
@@ -177,7 +185,8 @@ __global__ __launch_bounds__(64 * WM * WN, WM * WN == 8 ? 1 : 2) void conv_s32_k
   // same speed, tools/exp/conv_s32_dma.hip's history)
   constexpr int RS = 128;
   constexpr int A_BYTES = NPIX * RS, B_BYTES = BN * RS;
-  constexpr int MAIN_BYTES = (ADB ? 2 : 1) * A_BYTES + 2 * B_BYTES;
+  static_assert(!BREG || (T > 1 && WM == 1 && BN == 32 * WN && AIN == kInS32), "register-direct B: T > 1, 1 x WN waves");
+  constexpr int MAIN_BYTES = (ADB ? 2 : 1) * A_BYTES + (BREG ? 0 : 2 * B_BYTES);
   constexpr int TS = BN + 4;              // epilogue tile row stride (floats)
   constexpr int EPI_BYTES = BM * TS * 4;
   constexpr int LDS_BYTES = MAIN_BYTES > EPI_BYTES ? MAIN_BYTES : EPI_BYTES;
@@ -418,6 +427,70 @@ __global__ __launch_bounds__(64 * WM * WN, WM * WN == 8 ? 1 : 2) void conv_s32_k
     if (tid == 0) sImg[kImgZero] = 0.f;
     __syncthreads();
   }
+  if constexpr (BREG) {
+  // ---- register-direct B: the wave's channel tile of every step from the fragment-major weights ----
+  const __amdgpu_buffer_rsrc_t rsW =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(a.wf), (short)0, a.wbytes, 0x00020000);
+  const int wlane = ((n0 >> 5) + wn) * 4096 + lane * 16;
+  const int wstep = a.npad * 128;  // bytes per (group, tap) step
+  u32x4 bq0[4], bq1[4];            // ring: step i in bq(i & 1); [sub-step * 2 + (hi, lo)]
+  auto load_b = [&](u32x4 (&d)[4], int step) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) d[e] = __builtin_amdgcn_raw_buffer_load_b128(rsW, wlane + e * 1024, step * wstep, 0);
+  };
+#define OFLOW_READ_A(AH, AL, I, S_)                                                                                   \
+  {                                                                                                                  \
+    const int ii_ = (I);                                                                                              \
+    const int t_ = ii_ % T, ky_ = t_ / KW, kx_ = t_ - ky_ * KW;                                                       \
+    const int chi_ = 2 * (S_) + hh, clo_ = 4 + 2 * (S_) + hh;                                                        \
+    _Pragma("unroll") for (int mt_ = 0; mt_ < MT; ++mt_) {                                                           \
+      const int p_ = (mt_ + ky_) * HX + r + kx_;                                                                     \
+      const uint8_t* row_ = sA + p_ * RS;                                                                            \
+      AH[mt_] = *reinterpret_cast<const half8*>(row_ + ((chi_ ^ swz(p_)) << 4));                                     \
+      AL[mt_] = *reinterpret_cast<const half8*>(row_ + ((clo_ ^ swz(p_)) << 4));                                     \
+    }                                                                                                                \
+  }
+#define OFLOW_MFMAS_R(AH, AL, BC, S_)                                                                                 \
+  if (!OFLOW_ABL(2)) _Pragma("unroll") for (int mt = 0; mt < MT; ++mt) {                                             \
+    const half8 bh_ = __builtin_bit_cast(half8, BC[2 * (S_)]), bl_ = __builtin_bit_cast(half8, BC[2 * (S_) + 1]);     \
+    acc[mt][0] = __builtin_amdgcn_mfma_f32_32x32x16_f16(AH[mt], bl_, acc[mt][0], 0, 0, 0);                           \
+    acc[mt][0] = __builtin_amdgcn_mfma_f32_32x32x16_f16(AL[mt], bh_, acc[mt][0], 0, 0, 0);                           \
+    acc[mt][0] = __builtin_amdgcn_mfma_f32_32x32x16_f16(AH[mt], bh_, acc[mt][0], 0, 0, 0);                           \
+  }
+  load_b(bq0, 0);
+  load_b(bq1, S > 1 ? 1 : 0);
+  OFLOW_LOAD_A(ra, 0);
+  OFLOW_WRITE_A(ra, 0, 0);
+  OFLOW_LOAD_A(ra, a.kg > 1 ? 1 : 0);
+  __syncthreads();
+  half8 xah[MT], xal[MT], yah[MT], yal[MT];
+  OFLOW_READ_A(xah, xal, 0, 0);
+  // a loop body of an even number of steps keeps the ring slot of every step static: two groups when T is odd
+  constexpr int GPB = (T & 1) ? 2 : 1;
+  for (int g0 = 0; g0 < a.kg; g0 += GPB) {
+#pragma unroll
+    for (int j = 0; j < GPB * T; ++j) {
+      const int gg = g0 + j / T, t = j % T;
+      if (GPB == 2 && j == T && gg >= a.kg) break;  // odd group count: the last body has one group (uniform branch)
+      const int i_ = gg * T + t;
+      u32x4 (&bc)[4] = (j & 1) ? bq1 : bq0;
+      OFLOW_READ_A(yah, yal, i_, 1);
+      OFLOW_MFMAS_R(xah, xal, bc, 0);
+      if (t == T - 1) {  // the halo swap: every wave done reading A(g); A(g+1) visible before its first read
+        __syncthreads();
+        OFLOW_WRITE_A(ra, 0, gg + 1 < a.kg ? gg + 1 : gg);
+        const int g2 = gg + 2 < a.kg ? gg + 2 : a.kg - 1;
+        OFLOW_LOAD_A(ra, g2);
+        __syncthreads();
+      }
+      OFLOW_READ_A(xah, xal, i_ + 1, 0);
+      OFLOW_MFMAS_R(yah, yal, bc, 1);
+      load_b(bc, i_ + 2 < S ? i_ + 2 : S - 1);  // step i+2 into the slot step i used
+    }
+  }
+#undef OFLOW_READ_A
+#undef OFLOW_MFMAS_R
+  } else {
   // prologue: step 0 in LDS, step 1 in registers, sub-step 0 operands of step 0 read
   OFLOW_LOAD_B(rb, 0);
   OFLOW_LOAD_A(ra, 0);
@@ -470,6 +543,7 @@ __global__ __launch_bounds__(64 * WM * WN, WM * WN == 8 ? 1 : 2) void conv_s32_k
       OFLOW_MFMAS(yah, yal, ybh, ybl);
     }
   }
+  }  // LDS-staged B
 #undef OFLOW_MFMAS
 #undef OFLOW_READ_OPS
 #undef OFLOW_LOAD_A
@@ -758,9 +832,15 @@ __global__ __launch_bounds__(64 * WM * WN, WM * WN == 8 ? 1 : 2) void conv_s32_k
   }
 }
 
-template <int KH, int KW, int BN, int WM, int WN, int EPI, int TY = kTY>
+template <int KH, int KW, int BN, int WM, int WN, int EPI, int TY = kTY, bool BREG = false>
 int launch_conv(const ConvArgs& a0, hipStream_t s) {
   ConvArgs a = a0;
+  if constexpr (BREG) {
+    a.tiles_y = (a.H + TY - 1) / TY;
+    dim3 grid(a.tiles_x * a.tiles_y * a.B, a.npad / BN);
+    hipLaunchKernelGGL((conv_s32_kernel<KH, KW, BN, WM, WN, EPI, TY, kInS32, true>), grid, dim3(64 * WM * WN), 0, s, a);
+    return launch_status();
+  }
   a.tiles_y = (a.H + TY - 1) / TY;
   dim3 grid(a.tiles_x * a.tiles_y * a.B, a.npad / BN);
   if constexpr (KH == 3 && KW == 3 && EPI == 0) {  // the encoders' second block convs
@@ -807,9 +887,16 @@ inline bool small_grid(const ConvArgs& a, int bn) {
          bn >= 64;
 }
 
+// register-direct weights (BREG): 128-channel blocks of T > 1 convs on S32 input, given the fragment-major weights
+inline bool use_breg(const ConvArgs& a, int bn, int taps) {
+  return a.wf != nullptr && bn == 128 && taps > 1 && a.ain == kInS32 && a.stats == nullptr && !small_grid(a, bn);
+}
+
 template <int KH, int KW, int EPI>
 int launch_bn(const ConvArgs& a, int bn, hipStream_t s) {
   if (small_grid(a, bn)) return launch_conv<KH, KW, 64, 2, 2, EPI, 2>(a, s);
+  if constexpr (KH * KW > 1 && KH * KW != 4)  // (the 2x2 instance spills)
+    if (use_breg(a, bn, KH * KW)) return launch_conv<KH, KW, 128, 1, 4, EPI, kTY, true>(a, s);
   switch (bn) {
     case 128: return launch_conv<KH, KW, 128, 2, 2, EPI>(a, s);
     case 96: return launch_conv<KH, KW, 96, 4, 1, EPI>(a, s);
@@ -843,6 +930,10 @@ int dispatch_conv(const ConvArgs& a, int kh, int kw, int block_n, int epilogue, 
         if (key == 0x15) return launch_conv<1, 5, 64, 2, 2, 1, 2>(a, s);
         if (key == 0x51) return launch_conv<5, 1, 64, 2, 2, 1, 2>(a, s);
       }
+      if (use_breg(a, block_n, kh * kw)) {
+        if (key == 0x15) return launch_conv<1, 5, 128, 1, 4, 1, kTY, true>(a, s);
+        if (key == 0x51) return launch_conv<5, 1, 128, 1, 4, 1, kTY, true>(a, s);
+      }
       if (key == 0x15) return launch_conv<1, 5, 128, 2, 2, 1>(a, s);
       if (key == 0x51) return launch_conv<5, 1, 128, 2, 2, 1>(a, s);
       return OFLOW_E_SHAPE;
@@ -851,6 +942,10 @@ int dispatch_conv(const ConvArgs& a, int kh, int kw, int block_n, int epilogue, 
       if (small_grid(a, block_n)) {
         if (key == 0x15) return launch_conv<1, 5, 64, 2, 2, 2, 2>(a, s);
         if (key == 0x51) return launch_conv<5, 1, 64, 2, 2, 2, 2>(a, s);
+      }
+      if (use_breg(a, block_n, kh * kw)) {
+        if (key == 0x15) return launch_conv<1, 5, 128, 1, 4, 2, kTY, true>(a, s);
+        if (key == 0x51) return launch_conv<5, 1, 128, 1, 4, 2, kTY, true>(a, s);
       }
       if (key == 0x15) return launch_conv<1, 5, 128, 2, 2, 2>(a, s);
       if (key == 0x51) return launch_conv<5, 1, 128, 2, 2, 2>(a, s);
@@ -932,7 +1027,7 @@ OFLOW_RANGE_FLAG_SETTER(conv)
 
 using namespace oflow;
 
-extern "C" int oflow_conv_s32_ex3(const void* d_x, long long x_pixel_stride, int in_groups, const void* d_wpack,
+extern "C" int oflow_conv_s32_ex4(const void* d_x, long long x_pixel_stride, int in_groups, const void* d_wpack,
                                   int n_pad, const float* d_wscale, const float* d_bias, int N, int B, int H, int W, int kh,
                                   int kw, int block_n, int epilogue, int activation, float out_scale, void* d_y0,
                                   long long y0_pixel_stride, void* d_y1, long long y1_pixel_stride, float* d_f32,
@@ -940,7 +1035,7 @@ extern "C" int oflow_conv_s32_ex3(const void* d_x, long long x_pixel_stride, int
                                   float* d_gru_h, float* d_gru_z, int gru_channels, float* d_nhwc, int nhwc_pixel_stride,
                                   float* d_stats, const void* d_res, long long res_pixel_stride, int res_activation,
                                   int s2d, int in_format, const float* d_in_scale, const float* d_in_shift,
-                                  const float* d_addend, long long addend_pixel_stride, void* stream) {
+                                  const float* d_addend, long long addend_pixel_stride, const void* d_wfrag, void* stream) {
   ConvArgs a;
   const int st = build_conv_args(a, d_x, x_pixel_stride, in_groups, d_wpack, n_pad, d_wscale, d_bias, N, B, H, W, kh, kw,
                                  block_n, epilogue, activation, out_scale, d_y0, y0_pixel_stride, d_y1, y1_pixel_stride,
@@ -948,6 +1043,11 @@ extern "C" int oflow_conv_s32_ex3(const void* d_x, long long x_pixel_stride, int
                                  gru_channels, d_nhwc, nhwc_pixel_stride, d_stats, d_res, res_pixel_stride,
                                  res_activation, s2d);
   if (st != OFLOW_OK) return st;
+  if (d_wfrag) {  // the fragment-major copy of d_wpack (same size; n_pad a multiple of 32)
+    if ((uintptr_t)d_wfrag & 15) return OFLOW_E_ALIGN;
+    if (n_pad % 32) return OFLOW_E_SHAPE;
+    a.wf = static_cast<const uint8_t*>(d_wfrag);
+  }
   if (in_format < kInS32 || in_format > kInImg) return OFLOW_E_MODE;
   if (in_format == kInImg) {  // the stem from the image: 1x1 geometry over 5 patch groups, BN 64, epilogue 0
     if (kh != 1 || kw != 1 || epilogue != 0 || block_n != 64 || in_groups != (kImgK * kImgK * kImgC + 31) / 32)
@@ -982,6 +1082,22 @@ extern "C" int oflow_conv_s32_ex3(const void* d_x, long long x_pixel_stride, int
     a.addps = addend_pixel_stride;
   }
   return dispatch_conv(a, kh, kw, block_n, epilogue, static_cast<hipStream_t>(stream));
+}
+
+extern "C" int oflow_conv_s32_ex3(const void* d_x, long long x_pixel_stride, int in_groups, const void* d_wpack,
+                                  int n_pad, const float* d_wscale, const float* d_bias, int N, int B, int H, int W, int kh,
+                                  int kw, int block_n, int epilogue, int activation, float out_scale, void* d_y0,
+                                  long long y0_pixel_stride, void* d_y1, long long y1_pixel_stride, float* d_f32,
+                                  long long f32_batch_stride, long long f32_channel_stride, int f32_accumulate,
+                                  float* d_gru_h, float* d_gru_z, int gru_channels, float* d_nhwc, int nhwc_pixel_stride,
+                                  float* d_stats, const void* d_res, long long res_pixel_stride, int res_activation,
+                                  int s2d, int in_format, const float* d_in_scale, const float* d_in_shift,
+                                  const float* d_addend, long long addend_pixel_stride, void* stream) {
+  return oflow_conv_s32_ex4(d_x, x_pixel_stride, in_groups, d_wpack, n_pad, d_wscale, d_bias, N, B, H, W, kh, kw,
+                            block_n, epilogue, activation, out_scale, d_y0, y0_pixel_stride, d_y1, y1_pixel_stride,
+                            d_f32, f32_batch_stride, f32_channel_stride, f32_accumulate, d_gru_h, d_gru_z, gru_channels,
+                            d_nhwc, nhwc_pixel_stride, d_stats, d_res, res_pixel_stride, res_activation, s2d, in_format,
+                            d_in_scale, d_in_shift, d_addend, addend_pixel_stride, nullptr, stream);
 }
 
 extern "C" int oflow_conv_s32_ex2(const void* d_x, long long x_pixel_stride, int in_groups, const void* d_wpack,

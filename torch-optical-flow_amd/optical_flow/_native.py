@@ -68,6 +68,7 @@ SYMBOLS = (
     "oflow_corr_pyramid_tiled_s32",
     "oflow_flow_head2_s32",
     "oflow_conv_s32_ex3",
+    "oflow_conv_s32_ex4",
     "oflow_corr_fmap_grad_f32",
     "oflow_grid_warp_backward_f32",
     "oflow_grid_sample_backward_f32",
@@ -199,6 +200,8 @@ def load() -> ctypes.CDLL:
     lib.oflow_conv_s32_ex2.argtypes = list(lib.oflow_conv_s32_ex.argtypes[:-1]) + [I, P, P, P]
     lib.oflow_conv_s32_ex3.restype = I
     lib.oflow_conv_s32_ex3.argtypes = list(lib.oflow_conv_s32_ex2.argtypes[:-1]) + [P, L, P]
+    lib.oflow_conv_s32_ex4.restype = I
+    lib.oflow_conv_s32_ex4.argtypes = list(lib.oflow_conv_s32_ex3.argtypes[:-1]) + [P, P]
     lib.oflow_corr_lookup_backward_f32.restype = I
     lib.oflow_corr_lookup_backward_f32.argtypes = [P, P, I, I, I, I, PP, IP, IP, I, P]
     lib.oflow_corr_pyramid_grad_combine_f32.restype = I
@@ -554,6 +557,9 @@ def range_flag_raise_if_set(device: torch.device, what: str = "RAFT forward", al
 # reduction and one host sync per convolution. Off by default (the checked RAFT activations stay below ~1e3).
 CHECK_RANGE = os.environ.get("OFLOW_CHECK", "0") not in ("", "0")
 F16_MAX = 65504.0
+# conv_s32 passes the fragment-major weights (ConvWeights.frag) to the 128-channel multi-tap convolutions: their B
+# operand goes to registers straight from HBM / L2 instead of through LDS (csrc/conv_s32.hip, BREG). Bit-identical.
+CONV_BREG = os.environ.get("OFLOW_CONV_BREG", "1") not in ("", "0")
 
 
 def _range_check(x, what: str) -> None:
@@ -796,7 +802,7 @@ class ConvWeights:
     """A conv layer's weights packed for oflow_conv_s32: [in_groups][taps][n_pad][hi | lo] fp16 (per-output-channel
     power-of-two scaled so that max |w| = 2^14 keeps the lo halves normal), the inverse scales and the bias."""
 
-    __slots__ = ("pack", "wscale", "bias", "n", "n_pad", "kh", "kw", "kg", "layout", "cin")
+    __slots__ = ("pack", "wscale", "bias", "n", "n_pad", "kh", "kw", "kg", "layout", "cin", "_frag")
 
     def __init__(self, weight: torch.Tensor, bias, n_pad: int, patches: bool = False):
         w = weight.detach().float()
@@ -825,6 +831,20 @@ class ConvWeights:
         self.n, self.n_pad, self.kh, self.kw, self.kg = n, n_pad, kh, kw, kg
         self.cin = c  # real input channels (flop accounting)
         self.layout = "conv"  # "convc1_frag": convc1_level_weights (the fused lookup + convc1's fragment-major order)
+        self._frag = None
+        if t > 1 and n_pad % 32 == 0:  # built with the pack, never lazily inside a captured / timed forward
+            self.frag()
+
+    def frag(self) -> torch.Tensor:
+        """The pack reordered fragment-major for oflow_conv_s32_ex4's register-direct weights (include/oflow.h):
+        [kg][t][n_pad][hi, lo][k 32] -> [kg][t][n / 32][sub-step][hi, lo][k half][n % 32][8], built once."""
+        if self._frag is None:
+            if self.layout != "conv" or self.n_pad % 32:
+                raise RuntimeError("ConvWeights.frag: needs a conv-layout pack with n_pad a multiple of 32")
+            kg, t = self.pack.shape[:2]
+            f = self.pack.reshape(kg, t, self.n_pad // 32, 32, 2, 2, 2, 8)  # kg, t, ntile, r, hi/lo, sub, hh, 8
+            self._frag = f.permute(0, 1, 2, 5, 4, 6, 3, 7).contiguous()
+        return self._frag
 
 
 def convc1_level_weights(conv: torch.nn.Conv2d, num_levels: int, radius: int) -> "ConvWeights":
@@ -887,7 +907,7 @@ def conv_tiles(h: int, w: int) -> int:
 def conv_s32(x: S32Slice, cw: ConvWeights, block_n: int, act: str = "none", out_scale: float = 1.0, y0=None, y1=None,
              f32=None, f32_accumulate: bool = False, epilogue: int = 0, gru_h=None, gru_z=None, nhwc=None, stats=None,
              res=None, res_act: str = "none", s2d: bool = False, addend=None) -> None:
-    """Split-fp16 convolution (oflow_conv_s32_ex3). x: input S32Slice with cw.kg groups, or NhwcNormIn (3x3 only). y0/y1: S32Slice destinations
+    """Split-fp16 convolution (oflow_conv_s32_ex4). x: input S32Slice with cw.kg groups, or NhwcNormIn (3x3 only). y0/y1: S32Slice destinations
     (s2d: space-to-depth layout, half the spatial size). f32: (B, N', H, W) fp32 NCHW destination. nhwc: [P, N]
     fp32 destination. stats: instance-norm partials [B, conv_tiles(H, W), n_pad, 3]. res: S32Slice residual added
     after the activation, then res_act. epilogue 1/2: GRU gates / candidate with gru_h, gru_z ([P, CH] fp32);
@@ -934,13 +954,16 @@ def conv_s32(x: S32Slice, cw: ConvWeights, block_n: int, act: str = "none", out_
             raise RuntimeError(f"{what}: addend must be a GRU-epilogue fp32 [P, >= {cw.n}] view with 16-B aligned rows")
         ap, aps = addend.data_ptr(), addend.stride(0)
     dev = x.device
+    # register-direct weights for the 128-channel blocks of multi-tap convs on S32 input (the kernel ignores wf elsewhere)
+    wf = (cw.frag().data_ptr() if CONV_BREG and int(block_n) == 128 and cw.kh * cw.kw > 1 and not nin
+          and in_format == 0 and cw.layout == "conv" else None)
     if _flops is not None:
         taps, p_out = cw.kh * cw.kw, b * h * w  # (s2d only changes where the epilogue writes)
         n_exec = -(-cw.n_pad // int(block_n)) * int(block_n)
         _count(3 * 2 * p_out * n_exec * cw.kg * 32 * taps, 2 * p_out * cw.n * cw.cin * taps)
     with torch.cuda.device(dev), _Timed(f"conv{cw.kh}x{cw.kw}", dev):
         _check(
-            load().oflow_conv_s32_ex3(
+            load().oflow_conv_s32_ex4(
                 x.ptr, x.ps, cw.kg, cw.pack.data_ptr(), cw.n_pad, cw.wscale.data_ptr(),
                 cw.bias.data_ptr() if cw.bias is not None else None, cw.n, b, h, w, cw.kh, cw.kw, int(block_n),
                 int(epilogue), ACT[act], float(out_scale), y0.ptr if y0 is not None else None, y0.ps if y0 is not None else 0,
@@ -950,7 +973,7 @@ def conv_s32(x: S32Slice, cw: ConvWeights, block_n: int, act: str = "none", out_
                 stats.data_ptr() if stats is not None else None,
                 res.ptr if res is not None else None, res.ps if res is not None else 0, ACT[res_act], int(bool(s2d)),
                 in_format, x.scale.data_ptr() if nin else None, x.shift.data_ptr() if nin else None,
-                ap or None, aps, _stream(dev),
+                ap or None, aps, wf, _stream(dev),
             ),
             what,
         )
