@@ -124,8 +124,19 @@ def test_conv_s32_epilogues_slices_and_accumulate():
     assert float((coords.double() - (c0.double() + delta)).abs().max()) <= 1e-5
 
 
-def test_conv_s32_gru_epilogues():
-    """z|r gates and the candidate/blend epilogue against the SepConvGRU math (update.py:91-97)."""
+@pytest.mark.parametrize("flags", [0, 256])
+def test_conv_s32_gru_epilogues(flags):
+    """z|r gates and the candidate/blend epilogue against the SepConvGRU math (update.py:91-97); flags 256: the gates
+    from the hardware exp2 / reciprocal (sigmoid_hw / tanh_hw), same bound."""
+    lib = N.load()
+    lib.oflow_exp_set_conv_flags(flags)
+    try:
+        _gru_epilogues()
+    finally:
+        lib.oflow_exp_set_conv_flags(0)
+
+
+def _gru_epilogues():
     g = torch.Generator().manual_seed(11)
     b, h, w, ch = 2, 8, 36, 128
     hx = torch.randn(b, 384, h, w, generator=g).to(DEV)

@@ -52,7 +52,10 @@ def main():
                     "times with kernel parts dropped (exp_flags: 2 MFMAs, 4 A staging, 16 epilogue, 32 B staging, "
                     "64 main-loop barriers)")
     ap.add_argument("--shape-batch", type=int, default=0, help="override the batch (pairs) of --shape")
+    ap.add_argument("--conv-flags", type=int, default=0, help="oflow_exp_set_conv_flags value for the run (experiments)")
     args = ap.parse_args()
+    if args.conv_flags:
+        N.load().oflow_exp_set_conv_flags(args.conv_flags)
     b, h, w = SHAPES[args.shape]
     if args.shape_batch:
         b = args.shape_batch

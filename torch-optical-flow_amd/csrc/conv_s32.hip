@@ -101,6 +101,16 @@ constexpr int kImgC = 3, kImgK = 7, kImgRows = (kTY - 1) * 2 + kImgK, kImgCols =
 // 50 % of the stem's LDS cycles, profiles/r04/s1_pmc_mfma.json)
 constexpr int kImgHalf = (kImgCols + 1) / 2, kImgPitch = 2 * kImgHalf, kImgPlane = kImgRows * kImgPitch;
 
+// the GRU gates' sigmoid / tanh from the hardware exp2 and reciprocal (v_exp_f32, v_rcp_f32: 1 ulp each; a few
+// instructions instead of libm's expf + IEEE division / tanhf, ~25-30 VALU per value in an epilogue of 64 values per
+// lane). Absolute error <= ~2e-7 for both (tanh near 0 through 1 - 2 / (e^2v + 1)); NaN propagates, +-inf saturate.
+__device__ __forceinline__ float sigmoid_hw(float v) {
+  return __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(v * -1.4426950408889634f));
+}
+__device__ __forceinline__ float tanh_hw(float v) {
+  return 1.0f - 2.0f * __builtin_amdgcn_rcpf(__builtin_amdgcn_exp2f(v * 2.8853900817779268f) + 1.0f);
+}
+
 __device__ __forceinline__ float act_fn(float v, int act) {
   if (act == 1) return v < 0.f ? 0.f : v;  // relu; NaN propagates like ATen
   if (act == 2) return 1.0f / (1.0f + expf(-v));
@@ -184,7 +194,11 @@ __global__ __launch_bounds__(64 * WM * WN, WM * WN == 8 ? 1 : 2) void conv_s32_k
   // ds_read_b128 are bank-conflict free from any starting row (padded 144-B rows with affine addressing measured the
   // same speed, tools/exp/conv_s32_dma.hip's history)
   constexpr int RS = 128;
-  constexpr int A_BYTES = NPIX * RS, B_BYTES = BN * RS;
+  // BREG: the halo rows padded to 144 B instead of swizzled (consecutive rows start 36 banks apart: the 16 rows of a
+  // ds_read_b128 phase are conflict-free), so every A read is one per-lane base plus an immediate offset (the swizzle
+  // costs ~4 VALU per read, 16 reads per step with 4 row tiles per wave)
+  constexpr int RSA = BREG ? 144 : RS;
+  constexpr int A_BYTES = NPIX * RSA, B_BYTES = BN * RS;
   static_assert(!BREG || (T > 1 && WM == 1 && BN == 32 * WN && AIN == kInS32), "register-direct B: T > 1, 1 x WN waves");
   constexpr int MAIN_BYTES = (ADB ? 2 : 1) * A_BYTES + (BREG ? 0 : 2 * B_BYTES);
   constexpr int TS = BN + 4;              // epilogue tile row stride (floats)
@@ -212,6 +226,7 @@ __global__ __launch_bounds__(64 * WM * WN, WM * WN == 8 ? 1 : 2) void conv_s32_k
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave / WN, wn = wave % WN;
   const int r = lane & 31, hh = lane >> 5;
+  auto aswz = [](int p) { return BREG ? 0 : swz(p); };  // the halo rows' slot swizzle (none with padded rows)
 
   int tile = blockIdx.x;
   const int tx0 = (tile % a.tiles_x) * kTX;
@@ -311,11 +326,11 @@ __global__ __launch_bounds__(64 * WM * WN, WM * WN == 8 ? 1 : 2) void conv_s32_k
           }                                                                                                          \
           range_guard(mx_);                                                                                          \
         }                                                                                                            \
-        uint8_t* rw_ = sA + (BUF) * A_BYTES + p * RS + (c & 1) * 8;                                                  \
-        *reinterpret_cast<half4_*>(rw_ + (((c >> 1) ^ swz(p)) << 4)) = h4;                                           \
-        *reinterpret_cast<half4_*>(rw_ + (((4 + (c >> 1)) ^ swz(p)) << 4)) = l4;                                     \
+        uint8_t* rw_ = sA + (BUF) * A_BYTES + p * RSA + (c & 1) * 8;                                                 \
+        *reinterpret_cast<half4_*>(rw_ + (((c >> 1) ^ aswz(p)) << 4)) = h4;                                          \
+        *reinterpret_cast<half4_*>(rw_ + (((4 + (c >> 1)) ^ aswz(p)) << 4)) = l4;                                    \
       } else {                                                                                                       \
-        *reinterpret_cast<u32x4*>(sA + (BUF) * A_BYTES + p * RS + ((c ^ swz(p)) << 4)) =                            \
+        *reinterpret_cast<u32x4*>(sA + (BUF) * A_BYTES + p * RSA + ((c ^ aswz(p)) << 4)) =                          \
             ((aok >> s_) & 1u) ? RA[s_] : u32x4{0u, 0u, 0u, 0u};                                                     \
       }                                                                                                              \
     }                                                                                                                \
@@ -445,9 +460,9 @@ __global__ __launch_bounds__(64 * WM * WN, WM * WN == 8 ? 1 : 2) void conv_s32_k
     const int chi_ = 2 * (S_) + hh, clo_ = 4 + 2 * (S_) + hh;                                                        \
     _Pragma("unroll") for (int mt_ = 0; mt_ < MT; ++mt_) {                                                           \
       const int p_ = (mt_ + ky_) * HX + r + kx_;                                                                     \
-      const uint8_t* row_ = sA + p_ * RS;                                                                            \
-      AH[mt_] = *reinterpret_cast<const half8*>(row_ + ((chi_ ^ swz(p_)) << 4));                                     \
-      AL[mt_] = *reinterpret_cast<const half8*>(row_ + ((clo_ ^ swz(p_)) << 4));                                     \
+      const uint8_t* row_ = sA + p_ * RSA;                                                                           \
+      AH[mt_] = *reinterpret_cast<const half8*>(row_ + (chi_ << 4));                                                 \
+      AL[mt_] = *reinterpret_cast<const half8*>(row_ + (clo_ << 4));                                                 \
     }                                                                                                                \
   }
 #define OFLOW_MFMAS_R(AH, AL, BC, S_)                                                                                 \
@@ -741,6 +756,7 @@ __global__ __launch_bounds__(64 * WM * WN, WM * WN == 8 ? 1 : 2) void conv_s32_k
       pre[k][3] = zp[1];
     }
   }
+  const bool hwx = (a.exp_flags & 256) != 0;  // experiment: hardware exp2 / rcp gate functions
   constexpr int UNR = EPI == 0 ? 1 : KIT;  // GRU: unrolled (pre[k] in registers); EPI 0: a plain loop
   // where every item of a thread has the same channel octet (NTH a multiple of BN / 8), its (scale, bias) pairs are
   // read once: in the plain loop each item would otherwise wait on 8 dependent LDS round trips
@@ -808,11 +824,11 @@ __global__ __launch_bounds__(64 * WM * WN, WM * WN == 8 ? 1 : 2) void conv_s32_k
       if (n < a.gch) {
         float* zp = a.z + P * a.gch + n;
 #pragma unroll
-        for (int j = 0; j < 8; ++j) zp[j] = 1.0f / (1.0f + expf(-v[j]));
+        for (int j = 0; j < 8; ++j) zp[j] = hwx ? sigmoid_hw(v[j]) : 1.0f / (1.0f + expf(-v[j]));
       } else {
         float rh[8];
 #pragma unroll
-        for (int j = 0; j < 8; ++j) rh[j] = (1.0f / (1.0f + expf(-v[j]))) * pf[j];
+        for (int j = 0; j < 8; ++j) rh[j] = (hwx ? sigmoid_hw(v[j]) : 1.0f / (1.0f + expf(-v[j]))) * pf[j];
         store_s32(a.y0, a.y0ps, P, n - a.gch, a.gch, rh);
       }
     } else {
@@ -821,7 +837,7 @@ __global__ __launch_bounds__(64 * WM * WN, WM * WN == 8 ? 1 : 2) void conv_s32_k
       float hn[8];
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
-        const float q = tanhf(v[j]);
+        const float q = hwx ? tanh_hw(v[j]) : tanhf(v[j]);
         const float z = pf[8 + j];
         hn[j] = (1.0f - z) * pf[j] + z * q;
       }
