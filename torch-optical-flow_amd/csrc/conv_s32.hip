@@ -32,6 +32,12 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));  // native vector: stays in VGPRs (HIP uint4 is copied by memcpy)
 
 __device__ __forceinline__ int swz(int row) { return (row >> 1) & 7; }
+// operand rows in LDS: 144-B padded rows (1) or 128-B rows with XOR-swizzled 16-B slots (0; build with
+// VECFLAGS+=-DOFLOW_PAD_ROWS=0 for A/B). Both are conflict-free for the ds_read_b128 operand reads; the padded rows
+// make every read address one per-lane base plus an immediate (no per-read swizzle arithmetic).
+#ifndef OFLOW_PAD_ROWS
+#define OFLOW_PAD_ROWS 1
+#endif
 
 constexpr int kTY = 4, kTX = 32;  // default tile: kTY rows x kTX columns
 
@@ -197,8 +203,8 @@ __global__ __launch_bounds__(64 * WM * WN, WM * WN == 8 ? 1 : 2) void conv_s32_k
   // BREG: the halo rows padded to 144 B instead of swizzled (consecutive rows start 36 banks apart: the 16 rows of a
   // ds_read_b128 phase are conflict-free), so every A read is one per-lane base plus an immediate offset (the swizzle
   // costs ~4 VALU per read, 16 reads per step with 4 row tiles per wave)
-  constexpr int RSA = BREG ? 144 : RS;
-  constexpr int A_BYTES = NPIX * RSA, B_BYTES = BN * RS;
+  constexpr int RSA = (BREG || OFLOW_PAD_ROWS) ? 144 : RS, RSB = OFLOW_PAD_ROWS ? 144 : RS;
+  constexpr int A_BYTES = NPIX * RSA, B_BYTES = BN * RSB;
   static_assert(!BREG || (T > 1 && WM == 1 && BN == 32 * WN && AIN == kInS32), "register-direct B: T > 1, 1 x WN waves");
   constexpr int MAIN_BYTES = (ADB ? 2 : 1) * A_BYTES + (BREG ? 0 : 2 * B_BYTES);
   constexpr int TS = BN + 4;              // epilogue tile row stride (floats)
@@ -226,7 +232,8 @@ __global__ __launch_bounds__(64 * WM * WN, WM * WN == 8 ? 1 : 2) void conv_s32_k
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave / WN, wn = wave % WN;
   const int r = lane & 31, hh = lane >> 5;
-  auto aswz = [](int p) { return BREG ? 0 : swz(p); };  // the halo rows' slot swizzle (none with padded rows)
+  auto aswz = [](int p) { return (BREG || OFLOW_PAD_ROWS) ? 0 : swz(p); };  // row slot swizzles (none with padded rows)
+  auto bswz = [](int n) { return OFLOW_PAD_ROWS ? 0 : swz(n); };
 
   int tile = blockIdx.x;
   const int tx0 = (tile % a.tiles_x) * kTX;
@@ -346,7 +353,7 @@ __global__ __launch_bounds__(64 * WM * WN, WM * WN == 8 ? 1 : 2) void conv_s32_k
     const int item = tid + s_ * NTH;                                                                            \
     const int n = item >> 3, c = item & 7;                                                                           \
     if (BITEMS % NTH == 0 || item < BITEMS)                                                                     \
-      *reinterpret_cast<u32x4*>(sB + (BUF) * B_BYTES + n * RS + ((c ^ swz(n)) << 4)) = RB[s_];                      \
+      *reinterpret_cast<u32x4*>(sB + (BUF) * B_BYTES + n * RSB + ((c ^ bswz(n)) << 4)) = RB[s_];                    \
   }
   // operands of one 16-deep sub-step S_ of step I: A rows of this wave's pixel tiles at the step's tap offset, B rows
   // of its channel tiles; hi and lo halves
@@ -359,15 +366,15 @@ __global__ __launch_bounds__(64 * WM * WN, WM * WN == 8 ? 1 : 2) void conv_s32_k
     const int chi_ = 2 * (S_) + hh, clo_ = 4 + 2 * (S_) + hh;                                                        \
     _Pragma("unroll") for (int mt_ = 0; mt_ < MT; ++mt_) {                                                           \
       const int p_ = (wm * MT + mt_ + ky_) * HX + r + kx_;                                                           \
-      const uint8_t* row_ = bufA_ + p_ * RS;                                                                         \
-      AH[mt_] = *reinterpret_cast<const half8*>(row_ + ((chi_ ^ swz(p_)) << 4));                                     \
-      AL[mt_] = *reinterpret_cast<const half8*>(row_ + ((clo_ ^ swz(p_)) << 4));                                     \
+      const uint8_t* row_ = bufA_ + p_ * RSA;                                                                        \
+      AH[mt_] = *reinterpret_cast<const half8*>(row_ + ((chi_ ^ aswz(p_)) << 4));                                    \
+      AL[mt_] = *reinterpret_cast<const half8*>(row_ + ((clo_ ^ aswz(p_)) << 4));                                    \
     }                                                                                                                \
     _Pragma("unroll") for (int nt_ = 0; nt_ < NT; ++nt_) {                                                           \
       const int n_ = wn * (BN / WN) + nt_ * 32 + r;                                                                  \
-      const uint8_t* row_ = bufB_ + n_ * RS;                                                                         \
-      BH[nt_] = *reinterpret_cast<const half8*>(row_ + ((chi_ ^ swz(n_)) << 4));                                     \
-      BL[nt_] = *reinterpret_cast<const half8*>(row_ + ((clo_ ^ swz(n_)) << 4));                                     \
+      const uint8_t* row_ = bufB_ + n_ * RSB;                                                                        \
+      BH[nt_] = *reinterpret_cast<const half8*>(row_ + ((chi_ ^ bswz(n_)) << 4));                                    \
+      BL[nt_] = *reinterpret_cast<const half8*>(row_ + ((clo_ ^ bswz(n_)) << 4));                                    \
     }                                                                                                                \
   }
   // hi*lo + lo*hi + hi*hi per (pixel tile, channel tile): the lo*lo term is below fp32 rounding
