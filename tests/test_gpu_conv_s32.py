@@ -126,8 +126,8 @@ def test_conv_s32_epilogues_slices_and_accumulate():
 
 @pytest.mark.parametrize("flags", [0, 256])
 def test_conv_s32_gru_epilogues(flags):
-    """z|r gates and the candidate/blend epilogue against the SepConvGRU math (update.py:91-97); flags 256: the gates
-    from the hardware exp2 / reciprocal (sigmoid_hw / tanh_hw), same bound."""
+    """z|r gates and the candidate/blend epilogue against the SepConvGRU math (update.py:91-97): the default gates
+    (hardware exp2 / reciprocal, sigmoid_hw / tanh_hw) and, flags 256, libm's expf / tanhf; same bound."""
     lib = N.load()
     lib.oflow_exp_set_conv_flags(flags)
     try:
@@ -453,38 +453,48 @@ def test_flow_head_col2im_matches_fp64_and_conv(b, h, w):
     assert float((c1 - c2).abs().max()) <= 1e-4
 
 
-@pytest.mark.parametrize("kh,kw,cin,epi,b,h,w", [
-    (3, 3, 256, 0, 2, 70, 130),   # even group count
-    (3, 3, 352, 0, 1, 131, 131),  # odd group count with odd taps: the two-group loop body's one-group tail
-    (3, 3, 32, 0, 4, 45, 97),     # one group
-    (1, 5, 384, 1, 2, 66, 130),   # GRU z|r gates (epilogue 1)
-    (5, 1, 384, 2, 2, 66, 130),   # GRU candidate (epilogue 2)
-    (5, 1, 96, 0, 3, 61, 100),    # odd group count, odd taps
+@pytest.mark.parametrize("kh,kw,cin,n,bn,epi,stats,b,h,w", [
+    (3, 3, 256, 128, 128, 0, False, 2, 70, 130),   # even group count
+    (3, 3, 352, 128, 128, 0, False, 1, 131, 131),  # odd group count with odd taps: the two-group body's one-group tail
+    (3, 3, 32, 128, 128, 0, False, 4, 45, 97),     # one group
+    (1, 5, 384, 256, 128, 1, False, 2, 66, 130),   # GRU z|r gates (epilogue 1)
+    (5, 1, 384, 128, 128, 2, False, 2, 66, 130),   # GRU candidate (epilogue 2)
+    (5, 1, 96, 128, 128, 0, False, 3, 61, 100),    # odd group count, odd taps
+    (3, 3, 256, 192, 64, 0, False, 2, 55, 128),    # convc2's shape: 64-channel blocks (two-wave workgroups)
+    (3, 3, 64, 64, 64, 0, True, 2, 60, 96),        # an encoder layer-1 conv with instance-norm partials
+    (3, 3, 128, 128, 128, 0, True, 2, 27, 64),     # 128-channel blocks with partials
 ])
-def test_conv_register_weights_bit_identical(monkeypatch, kh, kw, cin, epi, b, h, w):
+def test_conv_register_weights_bit_identical(monkeypatch, kh, kw, cin, n, bn, epi, stats, b, h, w):
     """The register-direct weight path (ConvWeights.frag -> oflow_conv_s32_ex4, BREG kernels; grids over 16384 output
-    pixels at block_n 128) against the LDS-staged one: the same MFMAs in the same order per output, so every output
-    bit-identical; plus the fp64 bound of test_conv_s32_matches_fp64 for the plain epilogue."""
-    g = torch.Generator().manual_seed(kh * 100 + cin + epi)
+    pixels, or any grid with instance-norm partials, at block_n 128 / 64) against the LDS-staged one: the same MFMAs
+    in the same order per output, so every output and partial bit-identical; plus the fp64 bound of
+    test_conv_s32_matches_fp64 for the plain epilogue."""
+    g = torch.Generator().manual_seed(kh * 100 + cin + epi + n)
     x = (torch.randn(b, cin, h, w, generator=g) * 1.5).to(DEV)
-    n = 256 if epi == 1 else 128
     wt = (torch.randn(n, cin, kh, kw, generator=g) / math.sqrt(cin * kh * kw)).to(DEV)
     bias = torch.randn(n, generator=g).to(DEV)
-    cw = N.ConvWeights(wt, bias, n)
+    npad = -(-n // bn) * bn
+    cw = N.ConvWeights(wt, bias, npad)
     xs = N.s32_from_f32(x)
     ch = 128
 
     def run(breg):
         monkeypatch.setattr(N, "CONV_BREG", breg)
-        y = N.s32_empty(b, h, w, 4, DEV, zero=True)
+        y = N.s32_empty(b, h, w, -(-n // 32) if epi == 0 else 4, DEV, zero=True)
+        if stats:
+            raw = torch.zeros(b * h * w, n, device=DEV)
+            part = torch.zeros(b, N.conv_tiles(h, w), npad, 3, device=DEV)
+            N.conv_s32(N.S32Slice(xs), cw, bn, nhwc=raw, stats=part)
+            torch.cuda.synchronize()
+            return raw, part, None, None
         if epi == 0:
             f32 = torch.zeros(b, n, h, w, device=DEV)
-            N.conv_s32(N.S32Slice(xs), cw, 128, act="relu", y0=N.S32Slice(y), f32=f32)
+            N.conv_s32(N.S32Slice(xs), cw, bn, act="relu", y0=N.S32Slice(y), f32=f32)
             torch.cuda.synchronize()
             return f32, y, None, None
         hm = torch.tanh(torch.randn(b * h * w, ch, generator=torch.Generator().manual_seed(1))).to(DEV)
         z = torch.rand(b * h * w, ch, generator=torch.Generator().manual_seed(2)).to(DEV)
-        N.conv_s32(N.S32Slice(xs), cw, 128, epilogue=epi, y0=N.S32Slice(y), gru_h=hm, gru_z=z)
+        N.conv_s32(N.S32Slice(xs), cw, bn, epilogue=epi, y0=N.S32Slice(y), gru_h=hm, gru_z=z)
         torch.cuda.synchronize()
         return None, y, hm, z
 
@@ -492,7 +502,7 @@ def test_conv_register_weights_bit_identical(monkeypatch, kh, kw, cin, epi, b, h
     for u, v in zip(a, c):
         if u is not None:
             assert torch.equal(u, v)
-    if epi == 0:
+    if epi == 0 and not stats:
         ref, bound = _ref(N.s32_to_f32(xs, cin), wt, bias, kh, kw)
         err = (a[0].double() - torch.relu(ref)).abs()
         assert bool((err <= 2e-6 * bound + 1e-6).all()), float(err.max())

@@ -107,7 +107,7 @@ constexpr int kImgC = 3, kImgK = 7, kImgRows = (kTY - 1) * 2 + kImgK, kImgCols =
 // 50 % of the stem's LDS cycles, profiles/r04/s1_pmc_mfma.json)
 constexpr int kImgHalf = (kImgCols + 1) / 2, kImgPitch = 2 * kImgHalf, kImgPlane = kImgRows * kImgPitch;
 
-// the GRU gates' sigmoid / tanh from the hardware exp2 and reciprocal (v_exp_f32, v_rcp_f32: 1 ulp each; a few
+// the GRU gates' sigmoid / tanh (update.py:91-97) from the hardware exp2 and reciprocal (v_exp_f32, v_rcp_f32: 1 ulp each; a few
 // instructions instead of libm's expf + IEEE division / tanhf, ~25-30 VALU per value in an epilogue of 64 values per
 // lane). Absolute error <= ~2e-7 for both (tanh near 0 through 1 - 2 / (e^2v + 1)); NaN propagates, +-inf saturate.
 __device__ __forceinline__ float sigmoid_hw(float v) {
@@ -183,8 +183,8 @@ __device__ __forceinline__ void store_s32(uint8_t* y, long long ps, long long P,
 // instead of one barrier per step). No two waves load the same fragment. Same MFMAs in the same order per accumulator
 // as the LDS-staged kernel: bit-identical outputs.
 template <int KH, int KW, int BN, int WM, int WN, int EPI, int TY = kTY, int AIN = kInS32, bool BREG = false>
-__global__ __launch_bounds__(64 * WM * WN, WM * WN == 8 ? 1 : 2) void conv_s32_kernel(ConvArgs a) {
-  constexpr int NTH = 64 * WM * WN;  // 4 waves (two workgroups per CU) or 8 (one)
+__global__ __launch_bounds__(64 * WM * WN, WM * WN == 8 ? 1 : WM * WN == 2 ? 4 : 2) void conv_s32_kernel(ConvArgs a) {
+  constexpr int NTH = 64 * WM * WN;  // 4 waves (two workgroups per CU), 8 (one) or 2 (BREG 64-channel blocks: four)
   constexpr int T = KH * KW;
   constexpr int BM = TY * kTX;  // output pixels per workgroup (TY rows x 32 columns)
   constexpr int PH = KH / 2, PW = KW / 2;
@@ -193,7 +193,7 @@ __global__ __launch_bounds__(64 * WM * WN, WM * WN == 8 ? 1 : 2) void conv_s32_k
   constexpr int BITEMS = BN * 8, BPER = (BITEMS + NTH - 1) / NTH;
   constexpr int MT = TY / WM;            // 32-pixel row tiles per wave
   constexpr int NT = BN / WN / 32;        // 32-channel column tiles per wave
-  static_assert((WM * WN == 4 || WM * WN == 8) && MT >= 1 && NT >= 1, "bad wave grid");
+  static_assert((WM * WN == 4 || WM * WN == 8 || (BREG && WM * WN == 2)) && MT >= 1 && NT >= 1, "bad wave grid");
   // T == 1 (1x1 convs): the input tile changes every K-step, so A is staged like B (double buffered in LDS).
   constexpr bool ADB = (T == 1);
   // 128-B LDS rows, 16-B slots XOR-swizzled (slot ^= (row >> 1) & 7): the 32 rows of an MFMA operand read by
@@ -763,7 +763,9 @@ __global__ __launch_bounds__(64 * WM * WN, WM * WN == 8 ? 1 : 2) void conv_s32_k
       pre[k][3] = zp[1];
     }
   }
-  const bool hwx = (a.exp_flags & 256) != 0;  // experiment: hardware exp2 / rcp gate functions
+  // the gates from the hardware exp2 / reciprocal (default; in-process step A/B 19.31 -> 19.05 ms, flows within
+  // 2.8e-5 px, profiles/r04/s15_ab.log); exp flag 256: libm expf / tanhf and IEEE division (A/B only)
+  const bool hwx = (a.exp_flags & 256) == 0;
   constexpr int UNR = EPI == 0 ? 1 : KIT;  // GRU: unrolled (pre[k] in registers); EPI 0: a plain loop
   // where every item of a thread has the same channel octet (NTH a multiple of BN / 8), its (scale, bias) pairs are
   // read once: in the plain loop each item would otherwise wait on 8 dependent LDS round trips
@@ -863,7 +865,7 @@ int launch_conv(const ConvArgs& a0, hipStream_t s) {
     dim3 grid(a.tiles_x * a.tiles_y * a.B, a.npad / BN);
     hipLaunchKernelGGL((conv_s32_kernel<KH, KW, BN, WM, WN, EPI, TY, kInS32, true>), grid, dim3(64 * WM * WN), 0, s, a);
     return launch_status();
-  }
+  } else {
   a.tiles_y = (a.H + TY - 1) / TY;
   dim3 grid(a.tiles_x * a.tiles_y * a.B, a.npad / BN);
   if constexpr (KH == 3 && KW == 3 && EPI == 0) {  // the encoders' second block convs
@@ -887,6 +889,7 @@ int launch_conv(const ConvArgs& a0, hipStream_t s) {
   if (a.ain != kInS32) return OFLOW_E_MODE;
   hipLaunchKernelGGL((conv_s32_kernel<KH, KW, BN, WM, WN, EPI, TY>), grid, dim3(64 * WM * WN), 0, s, a);
   return launch_status();
+  }
 }
 
 // Small grids (batch 1 and other small images: under 16384 output pixels, e.g. every update-block conv of one Sintel
@@ -910,16 +913,21 @@ inline bool small_grid(const ConvArgs& a, int bn) {
          bn >= 64;
 }
 
-// register-direct weights (BREG): 128-channel blocks of T > 1 convs on S32 input, given the fragment-major weights
+// register-direct weights (BREG): 128- and 64-channel blocks of T > 1 convs on S32 input (instance-norm partials
+// included), given the fragment-major weights
 inline bool use_breg(const ConvArgs& a, int bn, int taps) {
-  return a.wf != nullptr && bn == 128 && taps > 1 && a.ain == kInS32 && a.stats == nullptr && !small_grid(a, bn);
+  return a.wf != nullptr && (bn == 128 || bn == 64) && taps > 1 && a.ain == kInS32 && !small_grid(a, bn);
 }
 
 template <int KH, int KW, int EPI>
 int launch_bn(const ConvArgs& a, int bn, hipStream_t s) {
   if (small_grid(a, bn)) return launch_conv<KH, KW, 64, 2, 2, EPI, 2>(a, s);
   if constexpr (KH * KW > 1 && KH * KW != 4)  // (the 2x2 instance spills)
-    if (use_breg(a, bn, KH * KW)) return launch_conv<KH, KW, 128, 1, 4, EPI, kTY, true>(a, s);
+    if (use_breg(a, bn, KH * KW)) {
+      if (bn == 128) return launch_conv<KH, KW, 128, 1, 4, EPI, kTY, true>(a, s);  // 4 waves x 32 channels
+      // 2 waves (four two-wave workgroups per CU); 3x3 only (the 1x5 / 5x1 instances need > 256 registers)
+      if constexpr (KH == 3 && KW == 3) return launch_conv<KH, KW, 64, 1, 2, EPI, kTY, true>(a, s);
+    }
   switch (bn) {
     case 128: return launch_conv<KH, KW, 128, 2, 2, EPI>(a, s);
     case 96: return launch_conv<KH, KW, 96, 4, 1, EPI>(a, s);
