@@ -183,8 +183,8 @@ __device__ __forceinline__ void store_s32(uint8_t* y, long long ps, long long P,
 // instead of one barrier per step). No two waves load the same fragment. Same MFMAs in the same order per accumulator
 // as the LDS-staged kernel: bit-identical outputs.
 template <int KH, int KW, int BN, int WM, int WN, int EPI, int TY = kTY, int AIN = kInS32, bool BREG = false>
-__global__ __launch_bounds__(64 * WM * WN, WM * WN == 8 ? 1 : WM * WN == 2 ? 4 : 2) void conv_s32_kernel(ConvArgs a) {
-  constexpr int NTH = 64 * WM * WN;  // 4 waves (two workgroups per CU), 8 (one) or 2 (BREG 64-channel blocks: four)
+__global__ __launch_bounds__(64 * WM * WN, WM * WN == 8 ? 1 : 2) void conv_s32_kernel(ConvArgs a) {
+  constexpr int NTH = 64 * WM * WN;  // 4 waves (two workgroups per CU) or 8 (one)
   constexpr int T = KH * KW;
   constexpr int BM = TY * kTX;  // output pixels per workgroup (TY rows x 32 columns)
   constexpr int PH = KH / 2, PW = KW / 2;
@@ -193,7 +193,7 @@ __global__ __launch_bounds__(64 * WM * WN, WM * WN == 8 ? 1 : WM * WN == 2 ? 4 :
   constexpr int BITEMS = BN * 8, BPER = (BITEMS + NTH - 1) / NTH;
   constexpr int MT = TY / WM;            // 32-pixel row tiles per wave
   constexpr int NT = BN / WN / 32;        // 32-channel column tiles per wave
-  static_assert((WM * WN == 4 || WM * WN == 8 || (BREG && WM * WN == 2)) && MT >= 1 && NT >= 1, "bad wave grid");
+  static_assert((WM * WN == 4 || WM * WN == 8) && MT >= 1 && NT >= 1, "bad wave grid");
   // T == 1 (1x1 convs): the input tile changes every K-step, so A is staged like B (double buffered in LDS).
   constexpr bool ADB = (T == 1);
   // 128-B LDS rows, 16-B slots XOR-swizzled (slot ^= (row >> 1) & 7): the 32 rows of an MFMA operand read by
@@ -913,21 +913,20 @@ inline bool small_grid(const ConvArgs& a, int bn) {
          bn >= 64;
 }
 
-// register-direct weights (BREG): 128- and 64-channel blocks of T > 1 convs on S32 input (instance-norm partials
-// included), given the fragment-major weights
+// register-direct weights (BREG): 128-channel blocks of T > 1 convs on S32 input, given the fragment-major weights.
+// r04 A/B (profiles/r04/s16_*): the same for 64-channel 3x3 blocks as two-wave workgroups (four per CU) was slower
+// (convc2 170 -> 179 us, convf2 35 -> 49 us alone; step -0.9 % instead of -4 %), and with instance-norm partials one
+// wave per 4-row sub-tile changes the partials' summation order (not bit-identical to the LDS-staged kernel): neither
+// kept.
 inline bool use_breg(const ConvArgs& a, int bn, int taps) {
-  return a.wf != nullptr && (bn == 128 || bn == 64) && taps > 1 && a.ain == kInS32 && !small_grid(a, bn);
+  return a.wf != nullptr && bn == 128 && taps > 1 && a.ain == kInS32 && a.stats == nullptr && !small_grid(a, bn);
 }
 
 template <int KH, int KW, int EPI>
 int launch_bn(const ConvArgs& a, int bn, hipStream_t s) {
   if (small_grid(a, bn)) return launch_conv<KH, KW, 64, 2, 2, EPI, 2>(a, s);
   if constexpr (KH * KW > 1 && KH * KW != 4)  // (the 2x2 instance spills)
-    if (use_breg(a, bn, KH * KW)) {
-      if (bn == 128) return launch_conv<KH, KW, 128, 1, 4, EPI, kTY, true>(a, s);  // 4 waves x 32 channels
-      // 2 waves (four two-wave workgroups per CU); 3x3 only (the 1x5 / 5x1 instances need > 256 registers)
-      if constexpr (KH == 3 && KW == 3) return launch_conv<KH, KW, 64, 1, 2, EPI, kTY, true>(a, s);
-    }
+    if (use_breg(a, bn, KH * KW)) return launch_conv<KH, KW, 128, 1, 4, EPI, kTY, true>(a, s);
   switch (bn) {
     case 128: return launch_conv<KH, KW, 128, 2, 2, EPI>(a, s);
     case 96: return launch_conv<KH, KW, 96, 4, 1, EPI>(a, s);

@@ -954,8 +954,8 @@ def conv_s32(x: S32Slice, cw: ConvWeights, block_n: int, act: str = "none", out_
             raise RuntimeError(f"{what}: addend must be a GRU-epilogue fp32 [P, >= {cw.n}] view with 16-B aligned rows")
         ap, aps = addend.data_ptr(), addend.stride(0)
     dev = x.device
-    # register-direct weights for the 128- / 64-channel blocks of multi-tap convs on S32 input (ignored elsewhere)
-    wf = (cw.frag().data_ptr() if CONV_BREG and int(block_n) in (64, 128) and cw.kh * cw.kw > 1 and not nin
+    # register-direct weights for the 128-channel blocks of multi-tap convs on S32 input (the kernel ignores wf elsewhere)
+    wf = (cw.frag().data_ptr() if CONV_BREG and int(block_n) == 128 and cw.kh * cw.kw > 1 and not nin
           and in_format == 0 and cw.layout == "conv" else None)
     if _flops is not None:
         taps, p_out = cw.kh * cw.kw, b * h * w  # (s2d only changes where the epilogue writes)
