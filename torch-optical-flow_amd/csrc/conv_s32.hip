@@ -35,6 +35,10 @@ __device__ __forceinline__ int swz(int row) { return (row >> 1) & 7; }
 // operand rows in LDS: 144-B padded rows (1) or 128-B rows with XOR-swizzled 16-B slots (0; build with
 // VECFLAGS+=-DOFLOW_PAD_ROWS=0 for A/B). Both are conflict-free for the ds_read_b128 operand reads; the padded rows
 // make every read address one per-lane base plus an immediate (no per-read swizzle arithmetic).
+// register-direct weights: steps of B fragments in flight (2 or 3; build with VECFLAGS+=-DOFLOW_BREG_RING=2 for A/B)
+#ifndef OFLOW_BREG_RING
+#define OFLOW_BREG_RING 3
+#endif
 #ifndef OFLOW_PAD_ROWS
 #define OFLOW_PAD_ROWS 1
 #endif
@@ -455,7 +459,11 @@ __global__ __launch_bounds__(64 * WM * WN, WM * WN == 8 ? 1 : 2) void conv_s32_k
       __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(a.wf), (short)0, a.wbytes, 0x00020000);
   const int wlane = ((n0 >> 5) + wn) * 4096 + lane * 16;
   const int wstep = a.npad * 128;  // bytes per (group, tap) step
-  u32x4 bq0[4], bq1[4];            // ring: step i in bq(i & 1); [sub-step * 2 + (hi, lo)]
+  // ring of RING steps' B fragments: step i in bq[i % RING]; [sub-step * 2 + (hi, lo)]. Vector-memory loads retire in
+  // issue order, so the loads of B issued after a group's halo prefetch (HBM latency) cannot be consumed before it:
+  // the ring depth is how many steps the prefetch has before a B wait covers it. 3 where the registers allow it.
+  constexpr int RING = (T == 5 && KH == 5 && EPI == 0) ? 2 : OFLOW_BREG_RING;  // (the 5x1 context conv: 255 VGPRs at 2)
+  u32x4 bq[RING][4];
   auto load_b = [&](u32x4 (&d)[4], int step) {
 #pragma unroll
     for (int e = 0; e < 4; ++e) d[e] = __builtin_amdgcn_raw_buffer_load_b128(rsW, wlane + e * 1024, step * wstep, 0);
@@ -479,23 +487,23 @@ __global__ __launch_bounds__(64 * WM * WN, WM * WN == 8 ? 1 : 2) void conv_s32_k
     acc[mt][0] = __builtin_amdgcn_mfma_f32_32x32x16_f16(AL[mt], bh_, acc[mt][0], 0, 0, 0);                           \
     acc[mt][0] = __builtin_amdgcn_mfma_f32_32x32x16_f16(AH[mt], bh_, acc[mt][0], 0, 0, 0);                           \
   }
-  load_b(bq0, 0);
-  load_b(bq1, S > 1 ? 1 : 0);
+#pragma unroll
+  for (int q = 0; q < RING; ++q) load_b(bq[q], q < S ? q : S - 1);
   OFLOW_LOAD_A(ra, 0);
   OFLOW_WRITE_A(ra, 0, 0);
   OFLOW_LOAD_A(ra, a.kg > 1 ? 1 : 0);
   __syncthreads();
   half8 xah[MT], xal[MT], yah[MT], yal[MT];
   OFLOW_READ_A(xah, xal, 0, 0);
-  // a loop body of an even number of steps keeps the ring slot of every step static: two groups when T is odd
-  constexpr int GPB = (T & 1) ? 2 : 1;
+  // a loop body of a multiple of RING steps keeps the ring slot of every step static: GPB groups per body
+  constexpr int GPB = (T % RING == 0) ? 1 : RING;  // (RING 2 or 3, both prime)
   for (int g0 = 0; g0 < a.kg; g0 += GPB) {
 #pragma unroll
     for (int j = 0; j < GPB * T; ++j) {
       const int gg = g0 + j / T, t = j % T;
-      if (GPB == 2 && j == T && gg >= a.kg) break;  // odd group count: the last body has one group (uniform branch)
+      if (GPB > 1 && j > 0 && t == 0 && gg >= a.kg) break;  // the last body's missing groups (uniform branch)
       const int i_ = gg * T + t;
-      u32x4 (&bc)[4] = (j & 1) ? bq1 : bq0;
+      u32x4 (&bc)[4] = bq[j % RING];
       OFLOW_READ_A(yah, yal, i_, 1);
       OFLOW_MFMAS_R(xah, xal, bc, 0);
       if (t == T - 1) {  // the halo swap: every wave done reading A(g); A(g+1) visible before its first read
@@ -507,7 +515,7 @@ __global__ __launch_bounds__(64 * WM * WN, WM * WN == 8 ? 1 : 2) void conv_s32_k
       }
       OFLOW_READ_A(xah, xal, i_ + 1, 0);
       OFLOW_MFMAS_R(yah, yal, bc, 1);
-      load_b(bc, i_ + 2 < S ? i_ + 2 : S - 1);  // step i+2 into the slot step i used
+      load_b(bc, i_ + RING < S ? i_ + RING : S - 1);  // step i+RING into the slot step i used
     }
   }
 #undef OFLOW_READ_A
