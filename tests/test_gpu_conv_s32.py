@@ -461,6 +461,8 @@ def test_flow_head_col2im_matches_fp64_and_conv(b, h, w):
     (5, 1, 384, 128, 128, 2, False, 2, 66, 130),   # GRU candidate (epilogue 2)
     (5, 1, 96, 128, 128, 0, False, 3, 61, 100),    # odd group count, odd taps
     (3, 3, 128, 128, 128, 0, True, 2, 27, 64),     # with instance-norm partials: the LDS-staged kernel (wf ignored)
+    (3, 3, 256, 192, 64, 0, False, 2, 55, 128),    # convc2's shape, 64-channel blocks (CONV_BREG64: 2 x 2 waves)
+    (3, 3, 96, 64, 64, 0, False, 3, 41, 133),      # 64-channel blocks, odd group count, ragged tiles
 ])
 def test_conv_register_weights_bit_identical(monkeypatch, kh, kw, cin, n, bn, epi, stats, b, h, w):
     """The register-direct weight path (ConvWeights.frag -> oflow_conv_s32_ex4, BREG kernels; grids over 16384 output
@@ -477,6 +479,7 @@ def test_conv_register_weights_bit_identical(monkeypatch, kh, kw, cin, n, bn, ep
 
     def run(breg):
         monkeypatch.setattr(N, "CONV_BREG", breg)
+        monkeypatch.setattr(N, "CONV_BREG64", breg)
         y = N.s32_empty(b, h, w, -(-n // 32) if epi == 0 else 4, DEV, zero=True)
         if stats:
             raw = torch.zeros(b * h * w, n, device=DEV)

@@ -35,9 +35,9 @@ __device__ __forceinline__ int swz(int row) { return (row >> 1) & 7; }
 // operand rows in LDS: 144-B padded rows (1) or 128-B rows with XOR-swizzled 16-B slots (0; build with
 // VECFLAGS+=-DOFLOW_PAD_ROWS=0 for A/B). Both are conflict-free for the ds_read_b128 operand reads; the padded rows
 // make every read address one per-lane base plus an immediate (no per-read swizzle arithmetic).
-// register-direct weights: steps of B fragments in flight (2 or 3; build with VECFLAGS+=-DOFLOW_BREG_RING=2 for A/B)
+// register-direct weights: steps of B fragments in flight (2 or 3: measured neutral, profiles/r04/s18_*; default 2)
 #ifndef OFLOW_BREG_RING
-#define OFLOW_BREG_RING 3
+#define OFLOW_BREG_RING 2
 #endif
 #ifndef OFLOW_PAD_ROWS
 #define OFLOW_PAD_ROWS 1
@@ -209,7 +209,8 @@ __global__ __launch_bounds__(64 * WM * WN, WM * WN == 8 ? 1 : 2) void conv_s32_k
   // costs ~4 VALU per read, 16 reads per step with 4 row tiles per wave)
   constexpr int RSA = (BREG || OFLOW_PAD_ROWS) ? 144 : RS, RSB = OFLOW_PAD_ROWS ? 144 : RS;
   constexpr int A_BYTES = NPIX * RSA, B_BYTES = BN * RSB;
-  static_assert(!BREG || (T > 1 && WM == 1 && BN == 32 * WN && AIN == kInS32), "register-direct B: T > 1, 1 x WN waves");
+  static_assert(!BREG || (T > 1 && (WM == 1 || WM == 2) && BN == 32 * WN && AIN == kInS32),
+                "register-direct B: T > 1, WM x WN waves of one 32-channel tile each");
   constexpr int MAIN_BYTES = (ADB ? 2 : 1) * A_BYTES + (BREG ? 0 : 2 * B_BYTES);
   constexpr int TS = BN + 4;              // epilogue tile row stride (floats)
   constexpr int EPI_BYTES = BM * TS * 4;
@@ -474,7 +475,7 @@ __global__ __launch_bounds__(64 * WM * WN, WM * WN == 8 ? 1 : 2) void conv_s32_k
     const int t_ = ii_ % T, ky_ = t_ / KW, kx_ = t_ - ky_ * KW;                                                       \
     const int chi_ = 2 * (S_) + hh, clo_ = 4 + 2 * (S_) + hh;                                                        \
     _Pragma("unroll") for (int mt_ = 0; mt_ < MT; ++mt_) {                                                           \
-      const int p_ = (mt_ + ky_) * HX + r + kx_;                                                                     \
+      const int p_ = (wm * MT + mt_ + ky_) * HX + r + kx_;                                                           \
       const uint8_t* row_ = sA + p_ * RSA;                                                                           \
       AH[mt_] = *reinterpret_cast<const half8*>(row_ + (chi_ << 4));                                                 \
       AL[mt_] = *reinterpret_cast<const half8*>(row_ + (clo_ << 4));                                                 \
@@ -927,14 +928,19 @@ inline bool small_grid(const ConvArgs& a, int bn) {
 // wave per 4-row sub-tile changes the partials' summation order (not bit-identical to the LDS-staged kernel): neither
 // kept.
 inline bool use_breg(const ConvArgs& a, int bn, int taps) {
-  return a.wf != nullptr && bn == 128 && taps > 1 && a.ain == kInS32 && a.stats == nullptr && !small_grid(a, bn);
+  return a.wf != nullptr && (bn == 128 || bn == 64) && taps > 1 && a.ain == kInS32 && a.stats == nullptr &&
+         !small_grid(a, bn);
 }
 
 template <int KH, int KW, int EPI>
 int launch_bn(const ConvArgs& a, int bn, hipStream_t s) {
   if (small_grid(a, bn)) return launch_conv<KH, KW, 64, 2, 2, EPI, 2>(a, s);
   if constexpr (KH * KW > 1 && KH * KW != 4)  // (the 2x2 instance spills)
-    if (use_breg(a, bn, KH * KW)) return launch_conv<KH, KW, 128, 1, 4, EPI, kTY, true>(a, s);
+    if (use_breg(a, bn, KH * KW)) {
+      if (bn == 128) return launch_conv<KH, KW, 128, 1, 4, EPI, kTY, true>(a, s);
+      // 64-channel blocks: 2 x 2 waves, each 2 row tiles x one 32-channel tile (3x3 only)
+      if constexpr (KH == 3 && KW == 3) return launch_conv<KH, KW, 64, 2, 2, EPI, kTY, true>(a, s);
+    }
   switch (bn) {
     case 128: return launch_conv<KH, KW, 128, 2, 2, EPI>(a, s);
     case 96: return launch_conv<KH, KW, 96, 4, 1, EPI>(a, s);

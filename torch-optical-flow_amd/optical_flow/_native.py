@@ -560,6 +560,8 @@ F16_MAX = 65504.0
 # conv_s32 passes the fragment-major weights (ConvWeights.frag) to the 128-channel multi-tap convolutions: their B
 # operand goes to registers straight from HBM / L2 instead of through LDS (csrc/conv_s32.hip, BREG). Bit-identical.
 CONV_BREG = os.environ.get("OFLOW_CONV_BREG", "1") not in ("", "0")
+# ... and to the 64-channel 3x3 blocks (2 x 2 waves, each two row tiles x one 32-channel tile)
+CONV_BREG64 = os.environ.get("OFLOW_CONV_BREG64", "0") not in ("", "0")
 
 
 def _range_check(x, what: str) -> None:
@@ -954,8 +956,10 @@ def conv_s32(x: S32Slice, cw: ConvWeights, block_n: int, act: str = "none", out_
             raise RuntimeError(f"{what}: addend must be a GRU-epilogue fp32 [P, >= {cw.n}] view with 16-B aligned rows")
         ap, aps = addend.data_ptr(), addend.stride(0)
     dev = x.device
-    # register-direct weights for the 128-channel blocks of multi-tap convs on S32 input (the kernel ignores wf elsewhere)
-    wf = (cw.frag().data_ptr() if CONV_BREG and int(block_n) == 128 and cw.kh * cw.kw > 1 and not nin
+    # register-direct weights for the 128- (and, CONV_BREG64, 64-) channel blocks of multi-tap convs on S32 input (the
+    # kernel ignores wf elsewhere)
+    wf = (cw.frag().data_ptr() if CONV_BREG and (int(block_n) == 128 or (CONV_BREG64 and int(block_n) == 64))
+          and cw.kh * cw.kw > 1 and not nin
           and in_format == 0 and cw.layout == "conv" else None)
     if _flops is not None:
         taps, p_out = cw.kh * cw.kw, b * h * w  # (s2d only changes where the epilogue writes)
