@@ -39,6 +39,10 @@ __device__ __forceinline__ int swz(int row) { return (row >> 1) & 7; }
 #ifndef OFLOW_BREG_RING
 #define OFLOW_BREG_RING 2
 #endif
+// register-direct weights, vertical taps: halo-row operands reused across taps (1; 0 = re-read per tap, for A/B)
+#ifndef OFLOW_VSLIDE
+#define OFLOW_VSLIDE 1
+#endif
 #ifndef OFLOW_PAD_ROWS
 #define OFLOW_PAD_ROWS 1
 #endif
@@ -494,10 +498,64 @@ __global__ __launch_bounds__(64 * WM * WN, WM * WN == 8 ? 1 : 2) void conv_s32_k
   OFLOW_WRITE_A(ra, 0, 0);
   OFLOW_LOAD_A(ra, a.kg > 1 ? 1 : 0);
   __syncthreads();
-  half8 xah[MT], xal[MT], yah[MT], yal[MT];
-  OFLOW_READ_A(xah, xal, 0, 0);
   // a loop body of a multiple of RING steps keeps the ring slot of every step static: GPB groups per body
   constexpr int GPB = (T % RING == 0) ? 1 : RING;  // (RING 2 or 3, both prime)
+  // Vertical taps (KH x 1): tap ky of row tile mt reads halo row mt + ky, so consecutive taps share MT - 1 of their MT
+  // rows: the operands live in registers per halo row and each step reads only its newest row (one row tile's 4 reads
+  // instead of MT's 16; LDS operand reads were ~30 of a GRU conv's ~145 us, profiles/r04/s18_abl.log).
+  constexpr bool VSLIDE = OFLOW_VSLIDE && KW == 1 && KH > 1 && WM == 1 && !(EPI == 0 && KH == 5);  // (5x1 EPI 0: VGPRs)
+  if constexpr (VSLIDE) {
+    constexpr int NR = MT + KH - 1;  // halo rows per group
+    half8 V[NR][2][2];               // [halo row][sub-step][hi, lo]
+    auto rd = [&](int hr, int sub) {
+      const uint8_t* row_ = sA + (hr * HX + r) * RSA;
+      V[hr][sub][0] = *reinterpret_cast<const half8*>(row_ + ((2 * sub + hh) << 4));
+      V[hr][sub][1] = *reinterpret_cast<const half8*>(row_ + ((4 + 2 * sub + hh) << 4));
+    };
+    auto mf = [&](int ky, int sub, u32x4 (&bc)[4]) {
+      if (OFLOW_ABL(2)) return;
+      const half8 bh_ = __builtin_bit_cast(half8, bc[2 * sub]), bl_ = __builtin_bit_cast(half8, bc[2 * sub + 1]);
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) {
+        acc[mt][0] = __builtin_amdgcn_mfma_f32_32x32x16_f16(V[mt + ky][sub][0], bl_, acc[mt][0], 0, 0, 0);
+        acc[mt][0] = __builtin_amdgcn_mfma_f32_32x32x16_f16(V[mt + ky][sub][1], bh_, acc[mt][0], 0, 0, 0);
+        acc[mt][0] = __builtin_amdgcn_mfma_f32_32x32x16_f16(V[mt + ky][sub][0], bh_, acc[mt][0], 0, 0, 0);
+      }
+    };
+#pragma unroll
+    for (int m = 0; m < MT; ++m) rd(m, 0);
+    for (int g0 = 0; g0 < a.kg; g0 += GPB) {
+#pragma unroll
+      for (int j = 0; j < GPB * T; ++j) {
+        const int gg = g0 + j / T, t = j % T;
+        if (GPB > 1 && j > 0 && t == 0 && gg >= a.kg) break;
+        const int i_ = gg * T + t;
+        u32x4 (&bc)[4] = bq[j % RING];
+        if (t == 0) {
+#pragma unroll
+          for (int m = 0; m < MT; ++m) rd(m, 1);
+        } else {
+          rd(t + MT - 1, 1);
+        }
+        mf(t, 0, bc);
+        if (t == T - 1) {
+          __syncthreads();
+          OFLOW_WRITE_A(ra, 0, gg + 1 < a.kg ? gg + 1 : gg);
+          const int g2 = gg + 2 < a.kg ? gg + 2 : a.kg - 1;
+          OFLOW_LOAD_A(ra, g2);
+          __syncthreads();
+#pragma unroll
+          for (int m = 0; m < MT; ++m) rd(m, 0);  // the next group's first tap (rows 0 .. MT-1: free since tap MT-1)
+        } else {
+          rd(t + MT, 0);  // the next tap's new row
+        }
+        mf(t, 1, bc);
+        load_b(bc, i_ + RING < S ? i_ + RING : S - 1);
+      }
+    }
+  } else {
+  half8 xah[MT], xal[MT], yah[MT], yal[MT];
+  OFLOW_READ_A(xah, xal, 0, 0);
   for (int g0 = 0; g0 < a.kg; g0 += GPB) {
 #pragma unroll
     for (int j = 0; j < GPB * T; ++j) {
@@ -519,6 +577,7 @@ __global__ __launch_bounds__(64 * WM * WN, WM * WN == 8 ? 1 : 2) void conv_s32_k
       load_b(bc, i_ + RING < S ? i_ + RING : S - 1);  // step i+RING into the slot step i used
     }
   }
+  }  // VSLIDE
 #undef OFLOW_READ_A
 #undef OFLOW_MFMAS_R
   } else {
