@@ -43,6 +43,10 @@ __device__ __forceinline__ int swz(int row) { return (row >> 1) & 7; }
 #ifndef OFLOW_VSLIDE
 #define OFLOW_VSLIDE 1
 #endif
+// XCD-aware workgroup order (1; 0 = 2D grid (tile, channel block), for A/B)
+#ifndef OFLOW_XCD_MAP
+#define OFLOW_XCD_MAP 1
+#endif
 #ifndef OFLOW_PAD_ROWS
 #define OFLOW_PAD_ROWS 1
 #endif
@@ -244,12 +248,32 @@ __global__ __launch_bounds__(64 * WM * WN, WM * WN == 8 ? 1 : 2) void conv_s32_k
   auto aswz = [](int p) { return (BREG || OFLOW_PAD_ROWS) ? 0 : swz(p); };  // row slot swizzles (none with padded rows)
   auto bswz = [](int n) { return OFLOW_PAD_ROWS ? 0 : swz(n); };
 
-  int tile = blockIdx.x;
+  // workgroup -> (tile, channel block). XCD-aware (OFLOW_XCD_MAP): workgroups are dealt round-robin over the 8 XCDs
+  // (each with its own L2), so ids 8 apart share one; the channel blocks of a tile take ids 8 apart within a group of
+  // 8 * nblk ids and run on one XCD close together in time -- the second reads the tile's halo from that L2 instead of
+  // from the fabric (a 2D grid runs every tile's block 0 before any block 1)
+  int tile, cblk;
+  if constexpr (OFLOW_XCD_MAP) {
+    const int nblk = a.npad / BN, ntiles = a.tiles_x * a.tiles_y * a.B, bid = blockIdx.x;
+    const int full = (ntiles >> 3) * 8 * nblk;
+    if (bid < full) {
+      const int grp = bid / (8 * nblk), rem = bid - grp * 8 * nblk;
+      cblk = rem >> 3;
+      tile = grp * 8 + (rem & 7);
+    } else {
+      const int ntail = ntiles & 7, rem = bid - full;
+      cblk = rem / ntail;
+      tile = (ntiles & ~7) + (rem - cblk * ntail);
+    }
+  } else {
+    tile = blockIdx.x;
+    cblk = blockIdx.y;
+  }
   const int tx0 = (tile % a.tiles_x) * kTX;
   tile /= a.tiles_x;
   const int ty0 = (tile % a.tiles_y) * TY;
   const int b = tile / a.tiles_y;
-  const int n0 = blockIdx.y * BN;
+  const int n0 = cblk * BN;
   const long long pix0 = (long long)b * a.H * a.W;
 
   // Register staging: one register set per operand; B(i+1) is written to LDS at step i's start and the set reloaded
@@ -925,17 +949,22 @@ __global__ __launch_bounds__(64 * WM * WN, WM * WN == 8 ? 1 : 2) void conv_s32_k
   }
 }
 
+inline dim3 conv_grid(const ConvArgs& a, int bn) {
+  const int ntiles = a.tiles_x * a.tiles_y * a.B;
+  return OFLOW_XCD_MAP ? dim3(ntiles * (a.npad / bn)) : dim3(ntiles, a.npad / bn);
+}
+
 template <int KH, int KW, int BN, int WM, int WN, int EPI, int TY = kTY, bool BREG = false>
 int launch_conv(const ConvArgs& a0, hipStream_t s) {
   ConvArgs a = a0;
   if constexpr (BREG) {
     a.tiles_y = (a.H + TY - 1) / TY;
-    dim3 grid(a.tiles_x * a.tiles_y * a.B, a.npad / BN);
+    dim3 grid = conv_grid(a, BN);
     hipLaunchKernelGGL((conv_s32_kernel<KH, KW, BN, WM, WN, EPI, TY, kInS32, true>), grid, dim3(64 * WM * WN), 0, s, a);
     return launch_status();
   } else {
   a.tiles_y = (a.H + TY - 1) / TY;
-  dim3 grid(a.tiles_x * a.tiles_y * a.B, a.npad / BN);
+  dim3 grid = conv_grid(a, BN);
   if constexpr (KH == 3 && KW == 3 && EPI == 0) {  // the encoders' second block convs
     if (a.ain == kInF32Norm) {
       hipLaunchKernelGGL((conv_s32_kernel<KH, KW, BN, WM, WN, EPI, TY, kInF32Norm>), grid, dim3(64 * WM * WN), 0, s, a);
