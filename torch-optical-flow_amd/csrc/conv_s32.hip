@@ -43,9 +43,11 @@ __device__ __forceinline__ int swz(int row) { return (row >> 1) & 7; }
 #ifndef OFLOW_VSLIDE
 #define OFLOW_VSLIDE 1
 #endif
-// XCD-aware workgroup order (1; 0 = 2D grid (tile, channel block), for A/B)
+// XCD-aware workgroup order (1) or the 2D grid (tile, channel block) (0, default): measured no faster -- per layer
+// alone 977.9 (2D) vs 986.8 us per update iteration, benches 422.0 / 423.4 vs 421.2 / 420.7 pairs/s alternated on one
+// box (profiles/r04/s21_*): the halo re-reads of a tile's second channel block already hit the Infinity Cache
 #ifndef OFLOW_XCD_MAP
-#define OFLOW_XCD_MAP 1
+#define OFLOW_XCD_MAP 0
 #endif
 #ifndef OFLOW_PAD_ROWS
 #define OFLOW_PAD_ROWS 1
