@@ -463,6 +463,7 @@ def test_flow_head_col2im_matches_fp64_and_conv(b, h, w):
     (3, 3, 128, 128, 128, 0, True, 2, 27, 64),     # with instance-norm partials: the LDS-staged kernel (wf ignored)
     (3, 3, 256, 192, 64, 0, False, 2, 55, 128),    # convc2's shape, 64-channel blocks (CONV_BREG64: 2 x 2 waves)
     (3, 3, 96, 64, 64, 0, False, 3, 41, 133),      # 64-channel blocks, odd group count, ragged tiles
+    (3, 3, 256, 2, 32, 0, False, 2, 55, 128),      # the flow head's output conv (CONV_BREG32: 4 x 1 waves)
 ])
 def test_conv_register_weights_bit_identical(monkeypatch, kh, kw, cin, n, bn, epi, stats, b, h, w):
     """The register-direct weight path (ConvWeights.frag -> oflow_conv_s32_ex4, BREG kernels; grids over 16384 output
@@ -480,6 +481,7 @@ def test_conv_register_weights_bit_identical(monkeypatch, kh, kw, cin, n, bn, ep
     def run(breg):
         monkeypatch.setattr(N, "CONV_BREG", breg)
         monkeypatch.setattr(N, "CONV_BREG64", breg)
+        monkeypatch.setattr(N, "CONV_BREG32", breg)
         y = N.s32_empty(b, h, w, -(-n // 32) if epi == 0 else 4, DEV, zero=True)
         if stats:
             raw = torch.zeros(b * h * w, n, device=DEV)

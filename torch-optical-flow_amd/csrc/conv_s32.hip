@@ -219,7 +219,7 @@ __global__ __launch_bounds__(64 * WM * WN, WM * WN == 8 ? 1 : 2) void conv_s32_k
   // costs ~4 VALU per read, 16 reads per step with 4 row tiles per wave)
   constexpr int RSA = (BREG || OFLOW_PAD_ROWS) ? 144 : RS, RSB = OFLOW_PAD_ROWS ? 144 : RS;
   constexpr int A_BYTES = NPIX * RSA, B_BYTES = BN * RSB;
-  static_assert(!BREG || (T > 1 && (WM == 1 || WM == 2) && BN == 32 * WN && AIN == kInS32),
+  static_assert(!BREG || (T > 1 && (WM == 1 || WM == 2 || WM == 4) && BN == 32 * WN && AIN == kInS32),
                 "register-direct B: T > 1, WM x WN waves of one 32-channel tile each");
   constexpr int MAIN_BYTES = (ADB ? 2 : 1) * A_BYTES + (BREG ? 0 : 2 * B_BYTES);
   constexpr int TS = BN + 4;              // epilogue tile row stride (floats)
@@ -1018,7 +1018,7 @@ inline bool small_grid(const ConvArgs& a, int bn) {
 // wave per 4-row sub-tile changes the partials' summation order (not bit-identical to the LDS-staged kernel): neither
 // kept.
 inline bool use_breg(const ConvArgs& a, int bn, int taps) {
-  return a.wf != nullptr && (bn == 128 || bn == 64) && taps > 1 && a.ain == kInS32 && a.stats == nullptr &&
+  return a.wf != nullptr && (bn == 128 || bn == 64 || bn == 32) && taps > 1 && a.ain == kInS32 && a.stats == nullptr &&
          !small_grid(a, bn);
 }
 
@@ -1029,7 +1029,12 @@ int launch_bn(const ConvArgs& a, int bn, hipStream_t s) {
     if (use_breg(a, bn, KH * KW)) {
       if (bn == 128) return launch_conv<KH, KW, 128, 1, 4, EPI, kTY, true>(a, s);
       // 64-channel blocks: 2 x 2 waves, each 2 row tiles x one 32-channel tile (3x3 only)
-      if constexpr (KH == 3 && KW == 3) return launch_conv<KH, KW, 64, 2, 2, EPI, kTY, true>(a, s);
+      if constexpr (KH == 3 && KW == 3) {
+        if (bn == 64) return launch_conv<KH, KW, 64, 2, 2, EPI, kTY, true>(a, s);
+        // 32-channel blocks (the flow head's 256 -> 2 output conv): 4 x 1 waves, one row tile each, all four loading
+        // the same B fragments (no per-step B staging or barrier)
+        return launch_conv<KH, KW, 32, 4, 1, EPI, kTY, true>(a, s);
+      }
     }
   switch (bn) {
     case 128: return launch_conv<KH, KW, 128, 2, 2, EPI>(a, s);

@@ -562,6 +562,8 @@ F16_MAX = 65504.0
 CONV_BREG = os.environ.get("OFLOW_CONV_BREG", "1") not in ("", "0")
 # ... and to the 64-channel 3x3 blocks (2 x 2 waves, each two row tiles x one 32-channel tile)
 CONV_BREG64 = os.environ.get("OFLOW_CONV_BREG64", "0") not in ("", "0")
+# ... and to the 32-channel 3x3 blocks (the flow head's output conv; 4 x 1 waves sharing the B fragments)
+CONV_BREG32 = os.environ.get("OFLOW_CONV_BREG32", "0") not in ("", "0")
 
 
 def _range_check(x, what: str) -> None:
@@ -958,7 +960,8 @@ def conv_s32(x: S32Slice, cw: ConvWeights, block_n: int, act: str = "none", out_
     dev = x.device
     # register-direct weights for the 128- (and, CONV_BREG64, 64-) channel blocks of multi-tap convs on S32 input (the
     # kernel ignores wf elsewhere)
-    wf = (cw.frag().data_ptr() if CONV_BREG and (int(block_n) == 128 or (CONV_BREG64 and int(block_n) == 64))
+    wf = (cw.frag().data_ptr() if CONV_BREG and (int(block_n) == 128 or (CONV_BREG64 and int(block_n) == 64)
+                                                 or (CONV_BREG32 and int(block_n) == 32))
           and cw.kh * cw.kw > 1 and not nin
           and in_format == 0 and cw.layout == "conv" else None)
     if _flops is not None:
