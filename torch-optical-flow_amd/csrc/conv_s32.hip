@@ -49,6 +49,9 @@ __device__ __forceinline__ int swz(int row) { return (row >> 1) & 7; }
 #ifndef OFLOW_XCD_MAP
 #define OFLOW_XCD_MAP 0
 #endif
+#ifndef OFLOW_STEM_SINGLE_A
+#define OFLOW_STEM_SINGLE_A 1
+#endif
 #ifndef OFLOW_PAD_ROWS
 #define OFLOW_PAD_ROWS 1
 #endif
@@ -209,7 +212,10 @@ __global__ __launch_bounds__(64 * WM * WN, WM * WN == 8 ? 1 : 2) void conv_s32_k
   constexpr int NT = BN / WN / 32;        // 32-channel column tiles per wave
   static_assert((WM * WN == 4 || WM * WN == 8) && MT >= 1 && NT >= 1, "bad wave grid");
   // T == 1 (1x1 convs): the input tile changes every K-step, so A is staged like B (double buffered in LDS).
-  constexpr bool ADB = (T == 1);
+  // The stem (kInImg) builds A from the image window already in LDS, so nothing is gained by building A(i+1) beside
+  // A(i): one A buffer and the halo-swap schedule (a barrier before each rebuild) -- 50.5 instead of 68.9 KB of LDS,
+  // three workgroups per CU instead of two (OFLOW_STEM_SINGLE_A=0: the double buffer, for A/B).
+  constexpr bool ADB = (T == 1) && !(AIN == kInImg && OFLOW_STEM_SINGLE_A);
   // 128-B LDS rows, 16-B slots XOR-swizzled (slot ^= (row >> 1) & 7): the 32 rows of an MFMA operand read by
   // ds_read_b128 are bank-conflict free from any starting row (padded 144-B rows with affine addressing measured the
   // same speed, tools/exp/conv_s32_dma.hip's history)
