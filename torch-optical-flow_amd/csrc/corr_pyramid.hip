@@ -123,6 +123,19 @@ __device__ __forceinline__ size_t lvl_off(const PyramidArgs& p, int l, size_t q,
   }
 }
 
+// TILED: a workgroup's first query's base pointer in level l (64-bit, once, in scalar registers) and 32-bit offsets
+// from it for its 128 queries (the per-store 64-bit index products were ~180 v_mul_lo_u32 / 86 v_mad_u64_u32 per
+// wave in the epilogue)
+__device__ __forceinline__ float* lvl_base(const PyramidArgs& p, int l, size_t q0) {
+  return p.lv[l] + q0 * (size_t)(p.HB[l] * p.WB[l] * 32);
+}
+__device__ __forceinline__ int lvl_off32(const PyramidArgs& p, int l, int dq, int y, int x) {
+  // 24-bit products (full-rate v_mul_u32_u24): dq < 128, a level's 4x8 tiles per query < 2^16 (checked on the host)
+  const unsigned t = __umul24(__umul24(static_cast<unsigned>(dq), static_cast<unsigned>(p.HB[l])) + (y >> 2),
+                              static_cast<unsigned>(p.WB[l])) + (x >> 3);
+  return static_cast<int>(t * 32u) + ((y & 3) << 3) + (x & 7);
+}
+
 // Workgroup -> (target tile, query block) for one image's Mt x Nt GEMM tiles, L2-aware: dispatch is round-robin over
 // the 8 XCDs (4 MB L2 each), so each XCD is given a contiguous run of the tile order, and the order walks bands of
 // kGM query blocks (A: kGM x 128 KB) across the target tiles (B: 256 KB each) -- the ~64 workgroups an XCD runs at
@@ -166,6 +179,7 @@ __device__ __forceinline__ void pyramid_epilogue(const PyramidArgs& p, f32x16 (&
     // 2 x 512 B (whole 128-B lines) instead of 8 scattered 32-B row pieces.
     float* sw = sbuf + wave * 2048;
     const int tb = p.WB[0] - (tx0 >> 3);  // tiles of this tile row that exist in the level (>= 1)
+    float* const L0b = lvl_base(p, 0, (size_t)b * Nn + i0);
     __syncthreads();  // the main loop's LDS operand reads are done (the scratch aliases them)
 #pragma unroll
     for (int ps = 0; ps < 4; ++ps) {
@@ -184,7 +198,7 @@ __device__ __forceinline__ void pyramid_epilogue(const PyramidArgs& p, f32x16 (&
         const int i = i0 + wave * 32 + 8 * ps + j;
         const float4 v = *reinterpret_cast<const float4*>(&sw[j * 256 + l0swz(tr * 128 + ch * 4)]);
         if (i < p.N && (y0 >> 2) < p.HB[0] && (ch >> 3) < tb)
-          *reinterpret_cast<float4*>(&p.lv[0][lvl_off<true>(p, 0, (size_t)b * Nn + i, y0, tx0) + ch * 4]) = v;
+          *reinterpret_cast<float4*>(&L0b[lvl_off32(p, 0, i - i0, y0, tx0) + ch * 4]) = v;
       }
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
       __builtin_amdgcn_wave_barrier();  // every lane's reads of this pass are done before the next pass overwrites
@@ -259,7 +273,7 @@ __device__ __forceinline__ void pyramid_epilogue(const PyramidArgs& p, f32x16 (&
       const int i = i0 + wave * 32 + ql;
       const float4 v = *reinterpret_cast<const float4*>(&sw[ql * 64 + ch * 4]);
       if (i < p.N && (y1 >> 2) < p.HB[1] && (ch >> 3) < tb1)
-        *reinterpret_cast<float4*>(&p.lv[1][lvl_off<true>(p, 1, (size_t)b * Nn + i, y1, tx0 >> 1) + ch * 4]) = v;
+        *reinterpret_cast<float4*>(&lvl_base(p, 1, (size_t)b * Nn + i0)[lvl_off32(p, 1, i - i0, y1, tx0 >> 1) + ch * 4]) = v;
     }
     if (p.nlev < 3) return;
     // levels 2 and 3 through LDS as well: per query, level 2 of this tile is 2 rows x 8 columns = 64 contiguous bytes
@@ -296,14 +310,14 @@ __device__ __forceinline__ void pyramid_epilogue(const PyramidArgs& p, f32x16 (&
       const int i = i0 + wave * 32 + ql;
       const float4 v = *reinterpret_cast<const float4*>(&s2[ql * 16 + part * 4]);
       if (i < p.N && (y2 >> 2) < p.HB[2] && (x2 >> 3) < p.WB[2])
-        *reinterpret_cast<float4*>(&p.lv[2][lvl_off<true>(p, 2, (size_t)b * Nn + i, y2, x2) + part * 4]) = v;
+        *reinterpret_cast<float4*>(&lvl_base(p, 2, (size_t)b * Nn + i0)[lvl_off32(p, 2, i - i0, y2, x2) + part * 4]) = v;
     }
     if (p.nlev >= 4 && lane < 32) {
       const int y3 = ty0 >> 3, x3 = tx0 >> 3;
       const int i = i0 + wave * 32 + lane;
       const float4 v = *reinterpret_cast<const float4*>(&s2[512 + lane * 4]);
       if (i < p.N && (y3 >> 2) < p.HB[3] && (x3 >> 3) < p.WB[3])
-        *reinterpret_cast<float4*>(&p.lv[3][lvl_off<true>(p, 3, (size_t)b * Nn + i, y3, x3)]) = v;
+        *reinterpret_cast<float4*>(&lvl_base(p, 3, (size_t)b * Nn + i0)[lvl_off32(p, 3, i - i0, y3, x3)]) = v;
     }
     return;
   }
@@ -577,6 +591,7 @@ static int corr_pyramid_impl(const float* d_fmap1, const float* d_fmap2, int B, 
     p.HB[l] = (p.Hl[l] + 3) / 4;
     p.WB[l] = (p.Wl[l] + 7) / 8;
   }
+  if ((long long)p.HB[0] * p.WB[0] >= (1ll << 17)) return OFLOW_E_SHAPE;  // lvl_off32's 24-bit products
   p.tiles_x = (W + kTC - 1) / kTC;
   p.scale = sqrtf(static_cast<float>(C));
   int e2 = 0;
@@ -638,6 +653,7 @@ extern "C" int oflow_corr_pyramid_tiled_s32(const void* d_fmap1_s32, const void*
     p.HB[l] = (p.Hl[l] + 3) / 4;
     p.WB[l] = (p.Wl[l] + 7) / 8;
   }
+  if ((long long)p.HB[0] * p.WB[0] >= (1ll << 17)) return OFLOW_E_SHAPE;  // lvl_off32's 24-bit products
   p.tiles_x = (W + kTC - 1) / kTC;
   p.scale = sqrtf(static_cast<float>(C));
   int e2 = 0;
