@@ -142,7 +142,6 @@ __device__ __forceinline__ float act_fn(float v, int act) {
 }
 
 __device__ __forceinline__ void split8(const float* v, half8& hi, half8& lo) {
-  range_guard8(v);
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
     _Float16 h_, l_;
@@ -152,25 +151,24 @@ __device__ __forceinline__ void split8(const float* v, half8& hi, half8& lo) {
   }
 }
 
-// store channels [n, n + 8) of pixel P (n % 8 == 0) into an S32 destination, only those < N
-__device__ __forceinline__ void store_s32(uint8_t* y, long long ps, long long P, int n, int N, const float* v) {
+// store channels [n, n + 8) of pixel P (n % 8 == 0) into an S32 destination, only those < N; the max |x| of the stored
+// values goes into gm (the caller range-guards once per epilogue: one branch instead of one per item)
+__device__ __forceinline__ void store_s32(uint8_t* y, long long ps, long long P, int n, int N, const float* v, float& gm) {
   uint8_t* line = y + P * ps + (long long)(n >> 5) * 128 + ((n & 31) >> 3) * 16;
   if (n + 8 <= N) {
     half8 hi, lo;
     split8(v, hi, lo);
+    gm = fmaxf(gm, fmaxf(fmaxf(fmaxf(fabsf(v[0]), fabsf(v[1])), fmaxf(fabsf(v[2]), fabsf(v[3]))),
+                         fmaxf(fmaxf(fabsf(v[4]), fabsf(v[5])), fmaxf(fabsf(v[6]), fabsf(v[7])))));
     *reinterpret_cast<half8*>(line) = hi;
     *reinterpret_cast<half8*>(line + 64) = lo;
   } else {
     _Float16* hp = reinterpret_cast<_Float16*>(line);
     _Float16* lp = reinterpret_cast<_Float16*>(line + 64);
-    float m = 0.f;
-#pragma unroll
-    for (int j = 0; j < 8; ++j)
-      if (n + j < N) m = fmaxf(m, fabsf(v[j]));
-    range_guard(m);
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       if (n + j < N) {
+        gm = fmaxf(gm, fabsf(v[j]));
         _Float16 h_, l_;
         split_f16(v[j], h_, l_);
         hp[j] = h_;
@@ -211,6 +209,7 @@ __global__ __launch_bounds__(64 * WM * WN, WM * WN == 8 ? 1 : 2) void conv_s32_k
   constexpr int MT = TY / WM;            // 32-pixel row tiles per wave
   constexpr int NT = BN / WN / 32;        // 32-channel column tiles per wave
   static_assert((WM * WN == 4 || WM * WN == 8) && MT >= 1 && NT >= 1, "bad wave grid");
+  static_assert(NTH % 8 == 0, "an A item's 16-B chunk is tid & 7");
   // T == 1 (1x1 convs): the input tile changes every K-step, so A is staged like B (double buffered in LDS).
   // The stem (kInImg) builds A from the image window already in LDS, so nothing is gained by building A(i+1) beside
   // A(i): one A buffer and the halo-swap schedule (a barrier before each rebuild) -- 50.5 instead of 68.9 KB of LDS,
@@ -330,8 +329,15 @@ __global__ __launch_bounds__(64 * WM * WN, WM * WN == 8 ? 1 : 2) void conv_s32_k
     else                                                                                                             \
       RA[s_] = __builtin_amdgcn_raw_buffer_load_b128(rsA, off_, (G) * 128, 0);                                      \
   }
+// (one range-guard branch per call: the max |x| of all the thread's split values; the normalising affine of the
+// thread's 4 channels read once: an item's chunk is tid & 7 for every item, NTH being a multiple of 8)
 #define OFLOW_WRITE_A(RA, BUF, G)                                                                                    \
-  if (!OFLOW_ABL(4)) _Pragma("unroll") for (int s_ = 0; s_ < APER; ++s_) {                                           \
+  if (!OFLOW_ABL(4)) {                                                                                               \
+  float amx_ = 0.f;                                                                                                  \
+  float2 af4_[4];                                                                                                    \
+  if constexpr (AIN == kInF32Norm) _Pragma("unroll") for (int e_ = 0; e_ < 4; ++e_)                                  \
+    af4_[e_] = sAff[(G) * 32 + 4 * (tid & 7) + e_];                                                                  \
+  _Pragma("unroll") for (int s_ = 0; s_ < APER; ++s_) {                                                              \
     const int item = tid + s_ * NTH;                                                                            \
     /* image input: consecutive lanes take consecutive pixels of one chunk (conflict-free window reads); else the   \
        8 chunks of a pixel (whole 128-B LDS rows per 8 lanes) */                                                     \
@@ -355,14 +361,14 @@ __global__ __launch_bounds__(64 * WM * WN, WM * WN == 8 ? 1 : 2) void conv_s32_k
             h4[e_] = hv;                                                                                             \
             l4[e_] = lv;                                                                                             \
           }                                                                                                          \
-          range_guard(mx_);                                                                                          \
+          amx_ = fmaxf(amx_, mx_);                                                                                   \
         } else if (((aok >> s_) & 1u) && (AIN != kInF32 || (G) * 32 + 4 * c < a.cin)) {                             \
           const float* fv = reinterpret_cast<const float*>(&RA[s_]);                                                 \
           float mx_ = 0.f;                                                                                           \
           _Pragma("unroll") for (int e_ = 0; e_ < 4; ++e_) {                                                         \
             float v_ = fv[e_];                                                                                       \
             if constexpr (AIN == kInF32Norm) {                                                                       \
-              const float2 af = sAff[(G) * 32 + 4 * c + e_];                                                         \
+              const float2 af = af4_[e_];                                                                            \
               v_ = v_ * af.x + af.y;                                                                                 \
               v_ = v_ < 0.f ? 0.f : v_;                                                                              \
             }                                                                                                        \
@@ -372,7 +378,7 @@ __global__ __launch_bounds__(64 * WM * WN, WM * WN == 8 ? 1 : 2) void conv_s32_k
             h4[e_] = hv;                                                                                             \
             l4[e_] = lv;                                                                                             \
           }                                                                                                          \
-          range_guard(mx_);                                                                                          \
+          amx_ = fmaxf(amx_, mx_);                                                                                   \
         }                                                                                                            \
         uint8_t* rw_ = sA + (BUF) * A_BYTES + p * RSA + (c & 1) * 8;                                                 \
         *reinterpret_cast<half4_*>(rw_ + (((c >> 1) ^ aswz(p)) << 4)) = h4;                                          \
@@ -382,6 +388,8 @@ __global__ __launch_bounds__(64 * WM * WN, WM * WN == 8 ? 1 : 2) void conv_s32_k
             ((aok >> s_) & 1u) ? RA[s_] : u32x4{0u, 0u, 0u, 0u};                                                     \
       }                                                                                                              \
     }                                                                                                                \
+  }                                                                                                                  \
+  if constexpr (AIN != kInS32) range_guard(amx_);                                                                    \
   }
 #define OFLOW_LOAD_B(RB, STEP)                                                                                       \
   _Pragma("unroll") for (int s_ = 0; s_ < BPER; ++s_) {                                                              \
@@ -867,6 +875,7 @@ __global__ __launch_bounds__(64 * WM * WN, WM * WN == 8 ? 1 : 2) void conv_s32_k
   // 2.8e-5 px, profiles/r04/s15_ab.log); exp flag 256: libm expf / tanhf and IEEE division (A/B only)
   const bool hwx = (a.exp_flags & 256) == 0;
   constexpr int UNR = EPI == 0 ? 1 : KIT;  // GRU: unrolled (pre[k] in registers); EPI 0: a plain loop
+  float gmx = 0.f;  // max |x| of every S32 value this thread stores (one range-guard branch, after the loop)
   // where every item of a thread has the same channel octet (NTH a multiple of BN / 8), its (scale, bias) pairs are
   // read once: in the plain loop each item would otherwise wait on 8 dependent LDS round trips
   constexpr bool FIXED_OCT = NTH % C8 == 0;
@@ -925,8 +934,8 @@ __global__ __launch_bounds__(64 * WM * WN, WM * WN == 8 ? 1 : 2) void conv_s32_k
           Pd = ((long long)b * H2 + (y >> 1)) * W2 + (x >> 1);
           nd = n + ((y & 1) * 2 + (x & 1)) * a.N;
         }
-        store_s32(a.y0, a.y0ps, Pd, nd, a.s2d ? 4 * a.N : a.N, v);
-        if (a.y1) store_s32(a.y1, a.y1ps, Pd, nd, a.s2d ? 4 * a.N : a.N, v);
+        store_s32(a.y0, a.y0ps, Pd, nd, a.s2d ? 4 * a.N : a.N, v, gmx);
+        if (a.y1) store_s32(a.y1, a.y1ps, Pd, nd, a.s2d ? 4 * a.N : a.N, v, gmx);
       }
     } else if constexpr (EPI == 1) {
       // [z | r] gates (update.py:91-96): z = sigmoid -> a.z; r*h = sigmoid(r) * h -> S32 y0 (channel n - gch)
@@ -938,7 +947,7 @@ __global__ __launch_bounds__(64 * WM * WN, WM * WN == 8 ? 1 : 2) void conv_s32_k
         float rh[8];
 #pragma unroll
         for (int j = 0; j < 8; ++j) rh[j] = (hwx ? sigmoid_hw(v[j]) : 1.0f / (1.0f + expf(-v[j]))) * pf[j];
-        store_s32(a.y0, a.y0ps, P, n - a.gch, a.gch, rh);
+        store_s32(a.y0, a.y0ps, P, n - a.gch, a.gch, rh, gmx);
       }
     } else {
       // candidate + blend (update.py:96-97): h = (1 - z) * h + z * tanh(q); h (fp32) in place + S32 y0
@@ -952,9 +961,10 @@ __global__ __launch_bounds__(64 * WM * WN, WM * WN == 8 ? 1 : 2) void conv_s32_k
       }
 #pragma unroll
       for (int j = 0; j < 8; ++j) hp[j] = hn[j];
-      store_s32(a.y0, a.y0ps, P, n, a.N, hn);
+      store_s32(a.y0, a.y0ps, P, n, a.N, hn, gmx);
     }
   }
+  range_guard(gmx);
 }
 
 inline dim3 conv_grid(const ConvArgs& a, int bn) {
