@@ -1023,6 +1023,9 @@ int g_conv_exp_flags = 0;
 // only). r02 adopted them from per-layer timings; in the step (concurrent streams) the 4-row tiles win: interleaved
 // in-process A/B 20.36 vs 20.53-20.55 ms (profiles/r03/exp/s9_ab_bn64.log).
 int g_bn64_8row = 0;
+// register-direct 128-channel convs with n_pad a multiple of 256 (GRU z|r, fh1) as 256-channel workgroups of 8 waves
+// (1 x 8, one per CU): the halo staged once for all 256 channels instead of once per 128-channel block (experiment)
+int g_breg256 = 0;
 inline bool small_grid(const ConvArgs& a, int bn) {
   return (long long)a.B * a.H * a.W < g_small_grid_px && a.stats == nullptr && a.ain == kInS32 && a.npad % 64 == 0 &&
          bn >= 64;
@@ -1043,6 +1046,7 @@ int launch_bn(const ConvArgs& a, int bn, hipStream_t s) {
   if (small_grid(a, bn)) return launch_conv<KH, KW, 64, 2, 2, EPI, 2>(a, s);
   if constexpr (KH * KW > 1 && KH * KW != 4)  // (the 2x2 instance spills)
     if (use_breg(a, bn, KH * KW)) {
+      if (bn == 128 && g_breg256 && a.npad % 256 == 0) return launch_conv<KH, KW, 256, 1, 8, EPI, kTY, true>(a, s);
       if (bn == 128) return launch_conv<KH, KW, 128, 1, 4, EPI, kTY, true>(a, s);
       // 64-channel blocks: 2 x 2 waves, each 2 row tiles x one 32-channel tile (3x3 only)
       if constexpr (KH == 3 && KW == 3) {
@@ -1086,6 +1090,10 @@ int dispatch_conv(const ConvArgs& a, int kh, int kw, int block_n, int epilogue, 
         if (key == 0x51) return launch_conv<5, 1, 64, 2, 2, 1, 2>(a, s);
       }
       if (use_breg(a, block_n, kh * kw)) {
+        if (g_breg256 && a.npad % 256 == 0) {
+          if (key == 0x15) return launch_conv<1, 5, 256, 1, 8, 1, kTY, true>(a, s);
+          if (key == 0x51) return launch_conv<5, 1, 256, 1, 8, 1, kTY, true>(a, s);
+        }
         if (key == 0x15) return launch_conv<1, 5, 128, 1, 4, 1, kTY, true>(a, s);
         if (key == 0x51) return launch_conv<5, 1, 128, 1, 4, 1, kTY, true>(a, s);
       }
@@ -1303,3 +1311,4 @@ extern "C" void oflow_exp_set_small_grid_px(int pixels) { oflow::g_small_grid_px
 extern "C" void oflow_exp_set_stats_8row(int on) { oflow::g_stats_8row = on; }
 extern "C" void oflow_exp_set_conv_flags(int flags) { oflow::g_conv_exp_flags = flags; }
 extern "C" void oflow_exp_set_bn64_8row(int on) { oflow::g_bn64_8row = on; }
+extern "C" void oflow_exp_set_breg256(int on) { oflow::g_breg256 = on; }
