@@ -516,9 +516,9 @@ def test_conv_register_weights_bit_identical(monkeypatch, kh, kw, cin, n, bn, ep
     (1, 5, 256, 1, 2, 55, 128),   # GRU z|r (epilogue 1), 1x5
     (5, 1, 352, 1, 1, 61, 100),   # 5x1, odd group count, ragged tiles
 ])
-def test_conv_register_weights_256_bit_identical(kh, kw, cin, epi, b, h, w):
-    """256-channel register-direct workgroups (8 waves, one per CU; experiment hook oflow_exp_set_breg256) against
-    the 128-channel ones: the same per-wave work and MFMA order, every output bit-identical."""
+def test_conv_register_weights_8wave_bit_identical(kh, kw, cin, epi, b, h, w):
+    """8-wave register-direct workgroups (2 x 4 waves of 2 row tiles; experiment hook oflow_exp_set_breg8w) against
+    the 4-wave ones (1 x 4 of 4 row tiles): the same MFMA order per accumulator, every output bit-identical."""
     g = torch.Generator().manual_seed(kh * 7 + cin + epi)
     x = (torch.randn(b, cin, h, w, generator=g) * 1.5).to(DEV)
     wt = (torch.randn(256, cin, kh, kw, generator=g) / math.sqrt(cin * kh * kw)).to(DEV)
@@ -527,7 +527,7 @@ def test_conv_register_weights_256_bit_identical(kh, kw, cin, epi, b, h, w):
     lib = N.load()
 
     def run(flag):
-        lib.oflow_exp_set_breg256(flag)
+        lib.oflow_exp_set_breg8w(flag)
         try:
             y = N.s32_empty(b, h, w, 8 if epi == 0 else 4, DEV, zero=True)
             if epi == 0:
@@ -541,7 +541,7 @@ def test_conv_register_weights_256_bit_identical(kh, kw, cin, epi, b, h, w):
             torch.cuda.synchronize()
             return z, y
         finally:
-            lib.oflow_exp_set_breg256(0)
+            lib.oflow_exp_set_breg8w(0)
 
     for u, v in zip(run(1), run(0)):
         assert torch.equal(u, v)
