@@ -510,38 +510,3 @@ def test_conv_register_weights_bit_identical(monkeypatch, kh, kw, cin, n, bn, ep
         assert bool((err <= 2e-6 * bound + 1e-6).all()), float(err.max())
 
 
-
-@pytest.mark.parametrize("kh,kw,cin,epi,b,h,w", [
-    (3, 3, 128, 0, 2, 55, 128),   # fh1's shape
-    (1, 5, 256, 1, 2, 55, 128),   # GRU z|r (epilogue 1), 1x5
-    (5, 1, 352, 1, 1, 61, 100),   # 5x1, odd group count, ragged tiles
-])
-def test_conv_register_weights_8wave_bit_identical(kh, kw, cin, epi, b, h, w):
-    """8-wave register-direct workgroups (2 x 4 waves of 2 row tiles; experiment hook oflow_exp_set_breg8w) against
-    the 4-wave ones (1 x 4 of 4 row tiles): the same MFMA order per accumulator, every output bit-identical."""
-    g = torch.Generator().manual_seed(kh * 7 + cin + epi)
-    x = (torch.randn(b, cin, h, w, generator=g) * 1.5).to(DEV)
-    wt = (torch.randn(256, cin, kh, kw, generator=g) / math.sqrt(cin * kh * kw)).to(DEV)
-    cw = N.ConvWeights(wt, torch.randn(256, generator=g).to(DEV), 256)
-    xs = N.s32_from_f32(x)
-    lib = N.load()
-
-    def run(flag):
-        lib.oflow_exp_set_breg8w(flag)
-        try:
-            y = N.s32_empty(b, h, w, 8 if epi == 0 else 4, DEV, zero=True)
-            if epi == 0:
-                f32 = torch.zeros(b, 256, h, w, device=DEV)
-                N.conv_s32(N.S32Slice(xs), cw, 128, act="relu", y0=N.S32Slice(y), f32=f32)
-                torch.cuda.synchronize()
-                return f32, y
-            hm = torch.tanh(torch.randn(b * h * w, 128, generator=torch.Generator().manual_seed(1))).to(DEV)
-            z = torch.empty(b * h * w, 128, device=DEV)
-            N.conv_s32(N.S32Slice(xs), cw, 128, epilogue=1, y0=N.S32Slice(y), gru_h=hm, gru_z=z)
-            torch.cuda.synchronize()
-            return z, y
-        finally:
-            lib.oflow_exp_set_breg8w(0)
-
-    for u, v in zip(run(1), run(0)):
-        assert torch.equal(u, v)

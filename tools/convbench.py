@@ -53,12 +53,9 @@ def main():
                     "64 main-loop barriers)")
     ap.add_argument("--shape-batch", type=int, default=0, help="override the batch (pairs) of --shape")
     ap.add_argument("--conv-flags", type=int, default=0, help="oflow_exp_set_conv_flags value for the run (experiments)")
-    ap.add_argument("--breg8w", action="store_true", help="oflow_exp_set_breg8w(1): 8-wave register-direct blocks")
     args = ap.parse_args()
     if args.conv_flags:
         N.load().oflow_exp_set_conv_flags(args.conv_flags)
-    if args.breg8w:
-        N.load().oflow_exp_set_breg8w(1)
     b, h, w = SHAPES[args.shape]
     if args.shape_batch:
         b = args.shape_batch

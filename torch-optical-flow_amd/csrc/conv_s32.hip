@@ -198,8 +198,8 @@ __device__ __forceinline__ void store_s32(uint8_t* y, long long ps, long long P,
 // instead of one barrier per step). No two waves load the same fragment. Same MFMAs in the same order per accumulator
 // as the LDS-staged kernel: bit-identical outputs.
 template <int KH, int KW, int BN, int WM, int WN, int EPI, int TY = kTY, int AIN = kInS32, bool BREG = false>
-// (the second bound is HIP's minimum waves per SIMD: 2 -> <= 256 VGPRs; 4 -> <= 128, two 8-wave workgroups per CU)
-__global__ __launch_bounds__(64 * WM * WN, WM * WN == 8 ? (BREG ? 4 : 1) : 2) void conv_s32_kernel(ConvArgs a) {
+// (the second bound is HIP's minimum waves per SIMD: 2 -> <= 256 VGPRs)
+__global__ __launch_bounds__(64 * WM * WN, WM * WN == 8 ? 1 : 2) void conv_s32_kernel(ConvArgs a) {
   constexpr int NTH = 64 * WM * WN;  // 4 waves (two workgroups per CU) or 8 (one)
   constexpr int T = KH * KW;
   constexpr int BM = TY * kTX;  // output pixels per workgroup (TY rows x 32 columns)
@@ -1024,12 +1024,11 @@ int g_conv_exp_flags = 0;
 // only). r02 adopted them from per-layer timings; in the step (concurrent streams) the 4-row tiles win: interleaved
 // in-process A/B 20.36 vs 20.53-20.55 ms (profiles/r03/exp/s9_ab_bn64.log).
 int g_bn64_8row = 0;
-// register-direct 128-channel blocks as 8 waves (2 x 4, each 2 row tiles x one 32-channel tile; <= 128 VGPRs, two
-// workgroups = four waves per SIMD) instead of 4 (1 x 4, 4 row tiles each, two waves per SIMD) (experiment hook).
-// r04 (profiles/r04/s26_*): 256-channel 8-wave workgroups (1 x 8, one per CU, the halo staged once for all 256
-// channels) were slower -- GRU z|r 139.6 / 138.0 -> 144.8 / 149.9 us, step 18.96 -> 19.74 ms: with one workgroup
-// per CU each halo-swap barrier idles the CU's matrix cores.
-int g_breg8w = 0;
+// r04 register-direct workgroup shapes measured against the 1 x 4 waves of 4 row tiles (bit-identical, not kept):
+// 256-channel 8-wave workgroups (1 x 8, one per CU, the halo staged once for all 256 channels): GRU z|r 139.6 / 138.0
+// -> 144.8 / 149.9 us, step 18.96 -> 19.74 ms (profiles/r04/s26_*) -- with one workgroup per CU each halo-swap
+// barrier idles the CU's matrix cores; 128-channel 8-wave workgroups (2 x 4 of 2 row tiles, <= 128 VGPRs, four waves
+// per SIMD): z|r 141.0 / 141.1 -> 148.9 / 150.3 us, step 19.07 -> 19.65 ms (s27_*).
 inline bool small_grid(const ConvArgs& a, int bn) {
   return (long long)a.B * a.H * a.W < g_small_grid_px && a.stats == nullptr && a.ain == kInS32 && a.npad % 64 == 0 &&
          bn >= 64;
@@ -1050,7 +1049,6 @@ int launch_bn(const ConvArgs& a, int bn, hipStream_t s) {
   if (small_grid(a, bn)) return launch_conv<KH, KW, 64, 2, 2, EPI, 2>(a, s);
   if constexpr (KH * KW > 1 && KH * KW != 4)  // (the 2x2 instance spills)
     if (use_breg(a, bn, KH * KW)) {
-      if (bn == 128 && g_breg8w) return launch_conv<KH, KW, 128, 2, 4, EPI, kTY, true>(a, s);
       if (bn == 128) return launch_conv<KH, KW, 128, 1, 4, EPI, kTY, true>(a, s);
       // 64-channel blocks: 2 x 2 waves, each 2 row tiles x one 32-channel tile (3x3 only)
       if constexpr (KH == 3 && KW == 3) {
@@ -1094,10 +1092,6 @@ int dispatch_conv(const ConvArgs& a, int kh, int kw, int block_n, int epilogue, 
         if (key == 0x51) return launch_conv<5, 1, 64, 2, 2, 1, 2>(a, s);
       }
       if (use_breg(a, block_n, kh * kw)) {
-        if (g_breg8w) {
-          if (key == 0x15) return launch_conv<1, 5, 128, 2, 4, 1, kTY, true>(a, s);
-          if (key == 0x51) return launch_conv<5, 1, 128, 2, 4, 1, kTY, true>(a, s);
-        }
         if (key == 0x15) return launch_conv<1, 5, 128, 1, 4, 1, kTY, true>(a, s);
         if (key == 0x51) return launch_conv<5, 1, 128, 1, 4, 1, kTY, true>(a, s);
       }
@@ -1315,4 +1309,3 @@ extern "C" void oflow_exp_set_small_grid_px(int pixels) { oflow::g_small_grid_px
 extern "C" void oflow_exp_set_stats_8row(int on) { oflow::g_stats_8row = on; }
 extern "C" void oflow_exp_set_conv_flags(int flags) { oflow::g_conv_exp_flags = flags; }
 extern "C" void oflow_exp_set_bn64_8row(int on) { oflow::g_bn64_8row = on; }
-extern "C" void oflow_exp_set_breg8w(int on) { oflow::g_breg8w = on; }
