@@ -113,8 +113,6 @@ struct ConvArgs {
   int wbytes;              // bytes of the packed weights (kg * taps * npad * 128)
   const uint8_t* wf;       // the same weights fragment-major (register-direct B, BREG kernels), or null
   int exp_flags;           // experiments only (oflow_exp_set_conv_flags): bit 0 = the stem's element-wise window loop
-  int stagger;             // experiments only (oflow_exp_set_conv_stagger): register-direct workgroups with bit 3 of
-                           // their id set start stagger x 1024 cycles late
 };
 // input formats of oflow_conv_s32_ex2
 constexpr int kInS32 = OFLOW_IN_S32, kInF32Norm = OFLOW_IN_F32_NORM, kInF32 = OFLOW_IN_F32, kInImg = OFLOW_IN_IMG7S2;
@@ -500,11 +498,6 @@ __global__ __launch_bounds__(64 * WM * WN, WM * WN == 8 ? 1 : 2) void conv_s32_k
     }
     if (tid == 0) sImg[kImgZero] = 0.f;
     __syncthreads();
-  }
-  if constexpr (BREG) {
-    if (a.stagger > 0 && ((blockIdx.x >> 3) & 1)) {  // experiment: offset co-resident workgroups' phases
-      for (int k = 0; k < a.stagger; ++k) __builtin_amdgcn_s_sleep(16);
-    }
   }
   if constexpr (BREG) {
   // ---- register-direct B: the wave's channel tile of every step from the fragment-major weights ----
@@ -1027,7 +1020,6 @@ int g_small_grid_px = 16384;  // output-pixel count under which the small tiles 
 // (profiles/r03/exp/s8b_ab_enc.log).
 int g_stats_8row = 0;
 int g_conv_exp_flags = 0;
-int g_conv_stagger = 0;
 // BN 64 convs without instance-norm partials (cnet's layer1, convc2, the motion conv) on 8-row tiles (experiments
 // only). r02 adopted them from per-layer timings; in the step (concurrent streams) the 4-row tiles win: interleaved
 // in-process A/B 20.36 vs 20.53-20.55 ms (profiles/r03/exp/s9_ab_bn64.log).
@@ -1186,7 +1178,6 @@ int build_conv_args(ConvArgs& a, const void* d_x, long long x_pixel_stride, int 
   if (wbytes >= (1ll << 31) || (long long)H * W * x_pixel_stride >= (1ll << 31)) return OFLOW_E_SHAPE;
   a.wbytes = static_cast<int>(wbytes);
   a.exp_flags = g_conv_exp_flags;
-  a.stagger = g_conv_stagger;
   (void)block_n;
   return OFLOW_OK;
 }
@@ -1317,5 +1308,4 @@ extern "C" int oflow_conv_s32(const void* d_x, long long x_pixel_stride, int in_
 extern "C" void oflow_exp_set_small_grid_px(int pixels) { oflow::g_small_grid_px = pixels; }
 extern "C" void oflow_exp_set_stats_8row(int on) { oflow::g_stats_8row = on; }
 extern "C" void oflow_exp_set_conv_flags(int flags) { oflow::g_conv_exp_flags = flags; }
-extern "C" void oflow_exp_set_conv_stagger(int n) { oflow::g_conv_stagger = n; }
 extern "C" void oflow_exp_set_bn64_8row(int on) { oflow::g_bn64_8row = on; }
