@@ -346,6 +346,25 @@ def test_graphed_forward_equals_eager():
             assert torch.equal(lo_g, lo_e) and torch.equal(up_g, up_e)
 
 
+def test_graphed_multi_pair_forward_equals_eager_two_lanes():
+    """GraphedRAFT on a multi-pair batch (3 pairs, above the flow-head threshold: the conv flow head) is captured with
+    one pair lane (the two-lane capture crashes in capture_end) and replays the eager two-lane forward's flows bit for
+    bit; the model's pair_lanes setting is restored after the capture."""
+    from model.graph import GraphedRAFT
+
+    model = _model(RAFT)
+    assert model.pair_lanes == 2
+    a0, a1 = synthetic.synthetic_pair(3, 436, 1024, seed=31)  # 3 x 55 x 128 = 21120 px: conv flow head, two lanes
+    padder = InputPadder(a0.shape)
+    p0, p1 = (x.to(DEV) for x in padder.pad(a0, a1))
+    with torch.inference_mode():
+        g = GraphedRAFT(model, p0, p1, iters=6)
+        assert model.pair_lanes == 2
+        lo_e, up_e = model(p0, p1, iters=6, test_mode=True)
+        lo_g, up_g = g(p0, p1)
+        assert torch.equal(lo_g, lo_e) and torch.equal(up_g, up_e)
+
+
 @pytest.mark.parametrize("where", ["images", "convc1", "convc2"])
 def test_range_guard_raises_on_split_overflow(where):
     """The split-fp16 range guard (oflow_set_range_flag): an activation whose fp16 hi half overflows (|x| >= 65520) sets

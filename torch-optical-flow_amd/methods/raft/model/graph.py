@@ -39,6 +39,19 @@ class GraphedRAFT:
         self.image0 = image0.detach().clone()
         self.image1 = image1.detach().clone()
         dev = image0.device
+        # multi-pair batches are captured with one pair lane: capturing the two-lane update loop (each lane with its
+        # own side stream) segfaults inside capture_end (profiles/r04/s12_graph8.log); one lane captures and replays
+        # bit-identically to the eager forward (tools/exp/graph_probe.py, 8 pairs: replay 19.72 ms vs eager two-lane
+        # 19.62 ms, profiles/r04/s32_graph8l1.log). The model's own setting is restored after the capture.
+        lanes = getattr(model, "pair_lanes", 1)
+        if image0.shape[0] > 1 and lanes > 1:
+            model.pair_lanes = 1
+        try:
+            self._capture(model, iters, warmup, dev)
+        finally:
+            model.pair_lanes = lanes
+
+    def _capture(self, model, iters: int, warmup: int, dev) -> None:
         with torch.inference_mode():
             side = torch.cuda.Stream(device=dev)
             side.wait_stream(torch.cuda.current_stream(dev))
