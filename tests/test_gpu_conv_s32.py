@@ -245,6 +245,29 @@ def test_pack_s32_and_flow_prep():
         assert float((N.s32_to_f32(t)[:, 382:] - flow).abs().max()) <= 1e-6 * float(flow.abs().max())
 
 
+@pytest.mark.parametrize("b,h,w", [(2, 11, 29), (4, 55, 128), (1, 47, 156), (3, 5, 3)])
+def test_flow_prep_tiled_equals_per_thread(b, h, w):
+    """The LDS-tiled flow_prep (default) against the per-thread form (experiment hook): patch matrix and the GRU inputs'
+    flow channels bit-identical, ragged tiles and images smaller than a tile included."""
+    g = torch.Generator().manual_seed(h * 100 + w)
+    coords = coords_grid(b, h, w, device=DEV) + (torch.randn(b, 2, h, w, generator=g) * 7).to(DEV)
+    lib = N.load()
+    outs = []
+    for untiled in (0, 1):
+        lib.oflow_exp_set_flow_prep_untiled(untiled)
+        try:
+            pm = N.s32_empty(b, h, w, 4, DEV, zero=True)
+            hx = N.s32_empty(b, h, w, 12, DEV, zero=True)
+            rhx = N.s32_empty(b, h, w, 12, DEV, zero=True)
+            N.flow_prep(coords, pm, (N.S32Slice(hx), 382), (N.S32Slice(rhx), 382))
+            torch.cuda.synchronize()
+            outs.append((pm, hx, rhx))
+        finally:
+            lib.oflow_exp_set_flow_prep_untiled(0)
+    for u, v in zip(*outs):
+        assert torch.equal(u, v)
+
+
 @pytest.mark.parametrize("c,n,bn", [(64, 64, 64), (96, 96, 96), (128, 128, 128)])
 def test_conv_normalise_on_load_equals_norm_apply(c, n, bn):
     """oflow_conv_s32_ex2 with a raw fp32 NHWC input normalised + ReLU'd while staged (NhwcNormIn) equals the

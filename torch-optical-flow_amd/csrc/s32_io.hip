@@ -121,6 +121,87 @@ __global__ __launch_bounds__(256) void flow_prep_kernel(const float* __restrict_
   }
 }
 
+// The same outputs from a 4 x 32-pixel tile per workgroup: the tile's flow window (10 x 38 pixels, flow = coords1 -
+// coords0 with zeros outside the image, the same fp32 subtraction as above) staged once in LDS, then each thread
+// builds one pixel's patch groups from it (lanes = consecutive pixels: conflict-free float2 reads). The per-thread
+// form above read its 49 taps' coordinates from global memory one dword at a time (2 x 16 loads per item): 24 us per
+// 4-pair launch in the step for 14 MB of output.
+constexpr int kFpTH = 4, kFpTW = 32, kFpWH = kFpTH + 6, kFpWW = kFpTW + 6;
+__global__ __launch_bounds__(256) void flow_prep_tiled_kernel(const float* __restrict__ coords, int B, int H, int W,
+                                                              int tiles_x, int tiles_y, uint8_t* pm, uint8_t* d0,
+                                                              long long d0ps, uint8_t* d1, long long d1ps) {
+  constexpr int KS = 7, R = 3, G = 4;
+  __shared__ float2 sF[kFpWH * kFpWW];
+  int t = blockIdx.x;
+  const int tx0 = (t % tiles_x) * kFpTW;
+  t /= tiles_x;
+  const int ty0 = (t % tiles_y) * kFpTH;
+  const int b = t / tiles_y;
+  const int HW = H * W;
+  const float* cx = coords + (long long)b * 2 * HW;
+  const float* cy = cx + HW;
+  for (int e = threadIdx.x; e < kFpWH * kFpWW; e += blockDim.x) {
+    const int wy = e / kFpWW, wx = e - wy * kFpWW;
+    const int yy = ty0 - R + wy, xx = tx0 - R + wx;
+    float2 f = make_float2(0.f, 0.f);
+    if (static_cast<unsigned>(yy) < static_cast<unsigned>(H) && static_cast<unsigned>(xx) < static_cast<unsigned>(W)) {
+      const int q = yy * W + xx;
+      f = make_float2(cx[q] - static_cast<float>(xx), cy[q] - static_cast<float>(yy));
+    }
+    sF[e] = f;
+  }
+  __syncthreads();
+  const int pl = threadIdx.x & (kFpTH * kFpTW - 1), py = pl / kFpTW, px = pl - py * kFpTW;
+  const int y = ty0 + py, x = tx0 + px;
+  if (y >= H || x >= W) return;
+  const long long p = (long long)b * HW + (long long)y * W + x;
+  float gm = 0.f;
+#pragma unroll
+  for (int gi = 0; gi < 2; ++gi) {
+    const int g = 2 * gi + (threadIdx.x >> 7);  // threads 0-127: groups 0, 2; 128-255: groups 1, 3
+    float v[32];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      const int tt = g * 16 + k;
+      float2 f = make_float2(0.f, 0.f);
+      if (tt < KS * KS) f = sF[(py + tt / KS) * kFpWW + px + tt % KS];
+      v[2 * k] = f.x;
+      v[2 * k + 1] = f.y;
+    }
+    uint8_t* line = pm + (p * G + g) * 128;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      half8 hi, lo;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        gm = fmaxf(gm, fabsf(v[8 * c + j]));
+        _Float16 h_, l_;
+        split_f16(v[8 * c + j], h_, l_);
+        hi[j] = h_;
+        lo[j] = l_;
+      }
+      *reinterpret_cast<half8*>(line + c * 16) = hi;
+      *reinterpret_cast<half8*>(line + c * 16 + 64) = lo;
+    }
+  }
+  range_guard(gm);  // (the centre tap is among the patch values: the flow channels below are covered)
+  if (threadIdx.x < 128 && d0) {
+    const float2 f = sF[(py + R) * kFpWW + px + R];
+    _Float16 hx, lx, hy, ly;
+    split_f16(f.x, hx, lx);
+    split_f16(f.y, hy, ly);
+    for (int d = 0; d < 2; ++d) {
+      uint8_t* dst = d == 0 ? d0 + p * d0ps : (d1 ? d1 + p * d1ps : nullptr);
+      if (!dst) continue;
+      _Float16* h = reinterpret_cast<_Float16*>(dst);
+      h[0] = hx;
+      h[1] = hy;
+      h[32] = lx;
+      h[33] = ly;
+    }
+  }
+}
+
 // Flow head output conv (update.py:35-36, `self.conv2`: 3x3, 256 -> 2, + coords1 in place, raft.py:133) for small
 // grids. Two output channels fill a matrix-core tile 1/16 (oflow_conv_s32 pads them to N = 32) and that conv's
 // LDS-staged K loop is latency-bound when the grid is one image (24.8 us at 55x128), so here the conv runs as fp32
@@ -261,6 +342,11 @@ extern "C" int oflow_pack_s32_f32(const float* d_x, long long x_batch_stride, in
   return launch_status();
 }
 
+namespace oflow {
+int g_flow_prep_untiled = 0;  // experiments only: the per-thread form (oflow_exp_set_flow_prep_untiled)
+}
+extern "C" void oflow_exp_set_flow_prep_untiled(int on) { oflow::g_flow_prep_untiled = on; }
+
 extern "C" int oflow_flow_prep_s32(const float* d_coords, int B, int H, int W, void* d_patches, void* d_flow0,
                                    long long flow0_pixel_stride, void* d_flow1, long long flow1_pixel_stride,
                                    void* stream) {
@@ -268,6 +354,16 @@ extern "C" int oflow_flow_prep_s32(const float* d_coords, int B, int H, int W, v
   if (B <= 0 || H <= 0 || W <= 0) return OFLOW_E_SHAPE;
   if (((uintptr_t)d_patches & 15) || (d_flow0 && ((uintptr_t)d_flow0 & 3)) || (d_flow1 && ((uintptr_t)d_flow1 & 3)))
     return OFLOW_E_ALIGN;
+  if ((long long)H * W >= (1ll << 31) / 2) return OFLOW_E_SHAPE;  // 32-bit pixel index within an image
+  if (!g_flow_prep_untiled) {
+    const int tiles_x = (W + kFpTW - 1) / kFpTW, tiles_y = (H + kFpTH - 1) / kFpTH;
+    const long long blocks = (long long)tiles_x * tiles_y * B;
+    if (blocks >= (1ll << 31)) return OFLOW_E_SHAPE;
+    hipLaunchKernelGGL(flow_prep_tiled_kernel, dim3((unsigned)blocks), dim3(256), 0, static_cast<hipStream_t>(stream),
+                       d_coords, B, H, W, tiles_x, tiles_y, static_cast<uint8_t*>(d_patches), static_cast<uint8_t*>(d_flow0),
+                       flow0_pixel_stride, static_cast<uint8_t*>(d_flow1), flow1_pixel_stride);
+    return launch_status();
+  }
   const long long items = (long long)B * H * W * 4;
   if ((items + 255) / 256 * 256 >= (1ll << 31)) return OFLOW_E_SHAPE;  // 32-bit indexing over the rounded-up grid
   hipLaunchKernelGGL(flow_prep_kernel, dim3((unsigned)((items + 255) / 256)), dim3(256), 0, static_cast<hipStream_t>(stream),
