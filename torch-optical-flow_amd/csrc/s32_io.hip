@@ -202,6 +202,26 @@ __global__ __launch_bounds__(256) void flow_prep_tiled_kernel(const float* __res
   }
 }
 
+// RAFT.forward's input scaling `2 * (image / 255.0) - 1.0` (methods/raft/model/raft.py:104-105) for both frames in
+// one pass (ATen runs it as three elementwise kernels per frame, on the step's critical path ahead of the encoders).
+// Same operations in the same order: a correctly rounded fp32 division, an exact doubling, a rounded subtraction.
+__global__ __launch_bounds__(256) void normalize_images_kernel(const float4* __restrict__ x0, const float4* __restrict__ x1,
+                                                               float4* __restrict__ y0, float4* __restrict__ y1,
+                                                               long long n4) {
+  const long long stride = (long long)gridDim.x * blockDim.x;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < 2 * n4; i += stride) {
+    const bool second = i >= n4;
+    const long long j = second ? i - n4 : i;
+    const float4 v = second ? x1[j] : x0[j];
+    float4 r;
+    r.x = 2.0f * (v.x / 255.0f) - 1.0f;
+    r.y = 2.0f * (v.y / 255.0f) - 1.0f;
+    r.z = 2.0f * (v.z / 255.0f) - 1.0f;
+    r.w = 2.0f * (v.w / 255.0f) - 1.0f;
+    (second ? y1 : y0)[j] = r;
+  }
+}
+
 // Flow head output conv (update.py:35-36, `self.conv2`: 3x3, 256 -> 2, + coords1 in place, raft.py:133) for small
 // grids. Two output channels fill a matrix-core tile 1/16 (oflow_conv_s32 pads them to N = 32) and that conv's
 // LDS-staged K loop is latency-bound when the grid is one image (24.8 us at 55x128), so here the conv runs as fp32
@@ -339,6 +359,20 @@ extern "C" int oflow_pack_s32_f32(const float* d_x, long long x_batch_stride, in
   hipLaunchKernelGGL(pack_s32_kernel, dim3((unsigned)((items + 255) / 256)), dim3(256), 0, static_cast<hipStream_t>(stream),
                      d_x, x_batch_stride, C, B, H * W, activation, dst_channel, static_cast<uint8_t*>(d_y0), y0_pixel_stride,
                      static_cast<uint8_t*>(d_y1), y1_pixel_stride, d_nhwc, nhwc_pixel_stride);
+  return launch_status();
+}
+
+extern "C" int oflow_normalize_images_f32(const float* d_x0, const float* d_x1, long long n, float* d_y0, float* d_y1,
+                                          void* stream) {
+  if (!d_x0 || !d_x1 || !d_y0 || !d_y1) return OFLOW_E_NULL;
+  if (n <= 0 || (n & 3)) return OFLOW_E_SHAPE;
+  if (((uintptr_t)d_x0 | (uintptr_t)d_x1 | (uintptr_t)d_y0 | (uintptr_t)d_y1) & 15) return OFLOW_E_ALIGN;
+  const long long n4 = n / 4;
+  const long long blocks = (2 * n4 + 255) / 256;
+  hipLaunchKernelGGL(normalize_images_kernel, dim3((unsigned)(blocks < 16384 ? blocks : 16384)), dim3(256), 0,
+                     static_cast<hipStream_t>(stream), reinterpret_cast<const float4*>(d_x0),
+                     reinterpret_cast<const float4*>(d_x1), reinterpret_cast<float4*>(d_y0), reinterpret_cast<float4*>(d_y1),
+                     n4);
   return launch_status();
 }
 

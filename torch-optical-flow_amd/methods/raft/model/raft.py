@@ -35,6 +35,10 @@ from .extractor import BasicEncoder, SplitEncoder
 from .update import BasicUpdateBlock, FusedUpdate, SplitUpdate, _side_stream
 from .utils import coords_grid, upflow8
 
+# RAFT.forward's input scaling (raft.py:104-105) through oflow_normalize_images_f32 (one kernel for both frames,
+# bit-identical) on GPU inference; False: the elementwise ATen form (A/B only)
+NATIVE_NORMALIZE = True
+
 
 class HParams(dict):
     """Attribute access to the constructor arguments (Lightning's ``self.hparams`` as used in `raft.py`)."""
@@ -285,8 +289,14 @@ class RAFT(nn.Module):
             self._range_pending = pend
 
     def _forward(self, image0: Tensor, image1: Tensor, iters: int, flow_init: Optional[Tensor], test_mode: bool):
-        image0 = (2 * (image0 / 255.0) - 1.0).contiguous()
-        image1 = (2 * (image1 / 255.0) - 1.0).contiguous()
+        if (NATIVE_NORMALIZE and image0.is_cuda and image1.is_cuda and image0.dtype == image1.dtype == torch.float32
+                and image0.shape == image1.shape
+                and not (torch.is_grad_enabled() and (image0.requires_grad or image1.requires_grad))):
+            # raft.py:104-105 as one kernel for both frames (bit-identical; ATen: three launches per frame)
+            image0, image1 = _native.normalize_images(image0, image1)
+        else:  # CPU tensors, or frames that need gradients (autograd through the elementwise form)
+            image0 = (2 * (image0 / 255.0) - 1.0).contiguous()
+            image1 = (2 * (image1 / 255.0) - 1.0).contiguous()
         hdim, cdim = self.hparams.hidden_dim, self.hparams.context_dim
 
         # the split encoders implement the inference forward: fnet in train mode with dropout > 0 applies Dropout2d in

@@ -69,6 +69,7 @@ SYMBOLS = (
     "oflow_flow_head2_s32",
     "oflow_conv_s32_ex3",
     "oflow_conv_s32_ex4",
+    "oflow_normalize_images_f32",
     "oflow_corr_fmap_grad_f32",
     "oflow_grid_warp_backward_f32",
     "oflow_grid_sample_backward_f32",
@@ -201,6 +202,8 @@ def load() -> ctypes.CDLL:
     lib.oflow_conv_s32_ex3.restype = I
     lib.oflow_conv_s32_ex3.argtypes = list(lib.oflow_conv_s32_ex2.argtypes[:-1]) + [P, L, P]
     lib.oflow_conv_s32_ex4.restype = I
+    lib.oflow_normalize_images_f32.restype = I
+    lib.oflow_normalize_images_f32.argtypes = [P, P, L, P, P, P]
     lib.oflow_conv_s32_ex4.argtypes = list(lib.oflow_conv_s32_ex3.argtypes[:-1]) + [P, P]
     lib.oflow_corr_lookup_backward_f32.restype = I
     lib.oflow_corr_lookup_backward_f32.argtypes = [P, P, I, I, I, I, PP, IP, IP, I, P]
@@ -1090,6 +1093,24 @@ def pack_s32(x: torch.Tensor, act: str, y0: S32Slice, y1=None, nhwc=None, dst_ch
             ),
             what,
         )
+
+
+def normalize_images(image0: torch.Tensor, image1: torch.Tensor):
+    """RAFT.forward's `2 * (image / 255.0) - 1.0` for both frames in one kernel (oflow_normalize_images_f32; the same
+    fp32 operations as the reference's, so bit-identical). Same-shape fp32 GPU tensors; returns new contiguous ones."""
+    what = "normalize_images"
+    x0 = _gpu_f32(image0, "image0", what).contiguous()
+    x1 = _gpu_f32(image1, "image1", what).contiguous()
+    if x0.shape != x1.shape or x0.device != x1.device:
+        raise RuntimeError(f"{what}: the frames must have the same shape and device")
+    y0, y1 = torch.empty_like(x0), torch.empty_like(x1)
+    n = x0.numel()
+    if n % 4 or x0.data_ptr() % 16 or x1.data_ptr() % 16:  # (views with odd offsets: the reference's elementwise form)
+        return (2 * (x0 / 255.0) - 1.0).contiguous(), (2 * (x1 / 255.0) - 1.0).contiguous()
+    with torch.cuda.device(x0.device):
+        _check(load().oflow_normalize_images_f32(x0.data_ptr(), x1.data_ptr(), n, y0.data_ptr(), y1.data_ptr(),
+                                                 _stream(x0.device)), what)
+    return y0, y1
 
 
 def flow_prep(coords: torch.Tensor, patches: torch.Tensor, flow0=None, flow1=None) -> None:
