@@ -201,8 +201,9 @@ int oflow_flow_prep_s32(const float* d_coords, int B, int H, int W, void* d_patc
  * followed by this gather. */
 int oflow_flow_head_col2im_f32(const float* d_y, const float* d_bias, int B, int H, int W, float* d_coords, void* stream);
 
-/* oflow_normalize_images_f32: y = 2 * (x / 255) - 1 for two frames of n fp32 values each (n a multiple of 4, 16-B
- * aligned): RAFT.forward's input scaling (methods/raft/model/raft.py:104-105), the same fp32 operations in one pass. */
+/* oflow_normalize_images_f32: y = 2 * (x / 255) - 1 for two frames of n fp32 values each (4-B aligned; vector loads
+ * when n % 4 == 0 and 16-B aligned): RAFT.forward's input scaling (methods/raft/model/raft.py:104-105), the reference's
+ * fp32 operations (a correctly rounded division) in one pass -- bit-identical to the reference on the CPU. */
 int oflow_normalize_images_f32(const float* d_x0, const float* d_x1, long long n, float* d_y0, float* d_y1, void* stream);
 
 /* oflow_set_range_flag: register d_flag (one unsigned int in device memory of the current device; NULL: off) as the

@@ -204,7 +204,10 @@ __global__ __launch_bounds__(256) void flow_prep_tiled_kernel(const float* __res
 
 // RAFT.forward's input scaling `2 * (image / 255.0) - 1.0` (methods/raft/model/raft.py:104-105) for both frames in
 // one pass (ATen runs it as three elementwise kernels per frame, on the step's critical path ahead of the encoders).
-// Same operations in the same order: a correctly rounded fp32 division, an exact doubling, a rounded subtraction.
+// The reference's operations in its order -- a correctly rounded fp32 division, an exact doubling, a rounded
+// subtraction -- so the result is bit-identical to the reference on the CPU; ATen on the GPU divides by a scalar as a
+// multiplication by fl(1/255), which differs from the true quotient in 1 ulp for ~74 % of the values
+// (profiles/r04/s36_div.log).
 __global__ __launch_bounds__(256) void normalize_images_kernel(const float4* __restrict__ x0, const float4* __restrict__ x1,
                                                                float4* __restrict__ y0, float4* __restrict__ y1,
                                                                long long n4) {
@@ -219,6 +222,18 @@ __global__ __launch_bounds__(256) void normalize_images_kernel(const float4* __r
     r.z = 2.0f * (v.z / 255.0f) - 1.0f;
     r.w = 2.0f * (v.w / 255.0f) - 1.0f;
     (second ? y1 : y0)[j] = r;
+  }
+}
+
+// any size / alignment: one element per thread-iteration
+__global__ __launch_bounds__(256) void normalize_images_scalar_kernel(const float* __restrict__ x0, const float* __restrict__ x1,
+                                                                      float* __restrict__ y0, float* __restrict__ y1,
+                                                                      long long n) {
+  const long long stride = (long long)gridDim.x * blockDim.x;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < 2 * n; i += stride) {
+    const bool second = i >= n;
+    const long long j = second ? i - n : i;
+    (second ? y1 : y0)[j] = 2.0f * ((second ? x1 : x0)[j] / 255.0f) - 1.0f;
   }
 }
 
@@ -365,8 +380,14 @@ extern "C" int oflow_pack_s32_f32(const float* d_x, long long x_batch_stride, in
 extern "C" int oflow_normalize_images_f32(const float* d_x0, const float* d_x1, long long n, float* d_y0, float* d_y1,
                                           void* stream) {
   if (!d_x0 || !d_x1 || !d_y0 || !d_y1) return OFLOW_E_NULL;
-  if (n <= 0 || (n & 3)) return OFLOW_E_SHAPE;
-  if (((uintptr_t)d_x0 | (uintptr_t)d_x1 | (uintptr_t)d_y0 | (uintptr_t)d_y1) & 15) return OFLOW_E_ALIGN;
+  if (n <= 0) return OFLOW_E_SHAPE;
+  if (((uintptr_t)d_x0 | (uintptr_t)d_x1 | (uintptr_t)d_y0 | (uintptr_t)d_y1) & 3) return OFLOW_E_ALIGN;
+  if ((n & 3) || (((uintptr_t)d_x0 | (uintptr_t)d_x1 | (uintptr_t)d_y0 | (uintptr_t)d_y1) & 15)) {
+    const long long blocks = (2 * n + 255) / 256;
+    hipLaunchKernelGGL(normalize_images_scalar_kernel, dim3((unsigned)(blocks < 16384 ? blocks : 16384)), dim3(256), 0,
+                       static_cast<hipStream_t>(stream), d_x0, d_x1, d_y0, d_y1, n);
+    return launch_status();
+  }
   const long long n4 = n / 4;
   const long long blocks = (2 * n4 + 255) / 256;
   hipLaunchKernelGGL(normalize_images_kernel, dim3((unsigned)(blocks < 16384 ? blocks : 16384)), dim3(256), 0,

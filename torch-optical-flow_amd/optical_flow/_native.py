@@ -1096,8 +1096,9 @@ def pack_s32(x: torch.Tensor, act: str, y0: S32Slice, y1=None, nhwc=None, dst_ch
 
 
 def normalize_images(image0: torch.Tensor, image1: torch.Tensor):
-    """RAFT.forward's `2 * (image / 255.0) - 1.0` for both frames in one kernel (oflow_normalize_images_f32; the same
-    fp32 operations as the reference's, so bit-identical). Same-shape fp32 GPU tensors; returns new contiguous ones."""
+    """RAFT.forward's `2 * (image / 255.0) - 1.0` for both frames in one kernel (oflow_normalize_images_f32: the
+    reference's fp32 operations with a correctly rounded division, bit-identical to the reference on the CPU -- ATen on
+    the GPU multiplies by fl(1/255) instead). Same-shape fp32 GPU tensors; returns new contiguous ones."""
     what = "normalize_images"
     x0 = _gpu_f32(image0, "image0", what).contiguous()
     x1 = _gpu_f32(image1, "image1", what).contiguous()
@@ -1105,8 +1106,6 @@ def normalize_images(image0: torch.Tensor, image1: torch.Tensor):
         raise RuntimeError(f"{what}: the frames must have the same shape and device")
     y0, y1 = torch.empty_like(x0), torch.empty_like(x1)
     n = x0.numel()
-    if n % 4 or x0.data_ptr() % 16 or x1.data_ptr() % 16:  # (views with odd offsets: the reference's elementwise form)
-        return (2 * (x0 / 255.0) - 1.0).contiguous(), (2 * (x1 / 255.0) - 1.0).contiguous()
     with torch.cuda.device(x0.device):
         _check(load().oflow_normalize_images_f32(x0.data_ptr(), x1.data_ptr(), n, y0.data_ptr(), y1.data_ptr(),
                                                  _stream(x0.device)), what)
