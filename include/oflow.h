@@ -206,6 +206,12 @@ int oflow_flow_head_col2im_f32(const float* d_y, const float* d_bias, int B, int
  * fp32 operations (a correctly rounded division) in one pass -- bit-identical to the reference on the CPU. */
 int oflow_normalize_images_f32(const float* d_x0, const float* d_x1, long long n, float* d_y0, float* d_y1, void* stream);
 
+/* oflow_replicate_pad_f32: InputPadder.pad (methods/raft/model/utils.py:38-61, F.pad(x, [left, right, top, bottom],
+ * mode="replicate")) of `count` (1..4) tensors of `planes` x H x W fp32 values each (host arrays of device pointers),
+ * into planes x (H + top + bottom) x (W + left + right): a copy, bit-exact, one launch. */
+int oflow_replicate_pad_f32(const float* const* d_src, float* const* d_dst, int count, long long planes, int H, int W,
+                            int top, int bottom, int left, int right, void* stream);
+
 /* oflow_set_range_flag: register d_flag (one unsigned int in device memory of the current device; NULL: off) as the
  * range flag of the split-fp16 operands. Every kernel that writes or stages S32 values (the conv epilogues and staging,
  * norm_apply, pack / flow_prep, the fused lookup + convc1) sets it to 1 (atomic or) when a value's hi half overflows

@@ -458,3 +458,19 @@ def test_normalize_images_bit_identical_to_reference(shape):
     x1.view(-1)[:6] = torch.tensor([0.0, 255.0, 1e-30, -0.0, 127.5, 3e38])
     y0, y1 = N.normalize_images(x0.to(DEV), x1.to(DEV))
     assert torch.equal(y0.cpu(), 2 * (x0 / 255.0) - 1.0) and torch.equal(y1.cpu(), 2 * (x1 / 255.0) - 1.0)
+
+
+@pytest.mark.parametrize("shape,mode", [((8, 3, 436, 1024), "sintel"), ((2, 3, 375, 1242), "kitti"),
+                                        ((1, 3, 61, 97), "sintel"), ((3, 2, 48, 64), "kitti")])
+def test_input_padder_native_pad_equals_f_pad(shape, mode):
+    """InputPadder.pad on GPU frames (oflow_replicate_pad_f32, all frames in one launch) against F.pad(mode='replicate')
+    (utils.py:38-61): bit-exact, both modes, ragged sizes, already-aligned sizes."""
+    import torch.nn.functional as F
+
+    g = torch.Generator().manual_seed(shape[2])
+    x0, x1 = (torch.rand(*shape, generator=g).to(DEV) * 255 for _ in range(2))
+    padder = InputPadder(shape, mode=mode)
+    p0, p1 = padder.pad(x0, x1)
+    assert torch.equal(p0, F.pad(x0, padder._pad, mode="replicate"))
+    assert torch.equal(p1, F.pad(x1, padder._pad, mode="replicate"))
+    assert torch.equal(padder.unpad(p0), x0)

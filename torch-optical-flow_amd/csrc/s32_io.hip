@@ -237,6 +237,41 @@ __global__ __launch_bounds__(256) void normalize_images_scalar_kernel(const floa
   }
 }
 
+// InputPadder.pad (methods/raft/model/utils.py:38-61, F.pad mode="replicate") of up to 4 same-shape tensors in one
+// launch: out[t][n][y][x] = in[t][n][clamp(y - top)][clamp(x - left)] -- a copy, bit-exact. One thread = 4 output
+// columns of one row (a 16-B store when the row pitch allows it).
+struct PadArgs {
+  const float* src[4];
+  float* dst[4];
+};
+__global__ __launch_bounds__(256) void replicate_pad_kernel(PadArgs a, int count, long long planes, int H, int W, int Ho,
+                                                            int Wo, int top, int left) {
+  const int qw = (Wo + 3) / 4;
+  const long long per = planes * Ho * qw;
+  const long long stride = (long long)gridDim.x * blockDim.x;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < per * count; i += stride) {
+    const int t = static_cast<int>(i / per);
+    long long r = i - t * per;
+    const int xq = static_cast<int>(r % qw);
+    r /= qw;
+    const int yo = static_cast<int>(r % Ho);
+    const long long n = r / Ho;
+    const int ys = min(max(yo - top, 0), H - 1);
+    const float* srow = a.src[t] + (n * H + ys) * W;
+    float* drow = a.dst[t] + (n * Ho + yo) * Wo;
+    float v[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) v[e] = srow[min(max(4 * xq + e - left, 0), W - 1)];
+    if ((Wo & 3) == 0 && (((uintptr_t)drow) & 15) == 0) {
+      *reinterpret_cast<float4*>(drow + 4 * xq) = make_float4(v[0], v[1], v[2], v[3]);
+    } else {
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        if (4 * xq + e < Wo) drow[4 * xq + e] = v[e];
+    }
+  }
+}
+
 // Flow head output conv (update.py:35-36, `self.conv2`: 3x3, 256 -> 2, + coords1 in place, raft.py:133) for small
 // grids. Two output channels fill a matrix-core tile 1/16 (oflow_conv_s32 pads them to N = 32) and that conv's
 // LDS-staged K loop is latency-bound when the grid is one image (24.8 us at 55x128), so here the conv runs as fp32
@@ -394,6 +429,25 @@ extern "C" int oflow_normalize_images_f32(const float* d_x0, const float* d_x1, 
                      static_cast<hipStream_t>(stream), reinterpret_cast<const float4*>(d_x0),
                      reinterpret_cast<const float4*>(d_x1), reinterpret_cast<float4*>(d_y0), reinterpret_cast<float4*>(d_y1),
                      n4);
+  return launch_status();
+}
+
+extern "C" int oflow_replicate_pad_f32(const float* const* d_src, float* const* d_dst, int count, long long planes, int H,
+                                       int W, int top, int bottom, int left, int right, void* stream) {
+  if (!d_src || !d_dst) return OFLOW_E_NULL;
+  if (count < 1 || count > 4 || planes <= 0 || H <= 0 || W <= 0 || top < 0 || bottom < 0 || left < 0 || right < 0)
+    return OFLOW_E_SHAPE;
+  PadArgs a{};
+  for (int t = 0; t < count; ++t) {
+    if (!d_src[t] || !d_dst[t]) return OFLOW_E_NULL;
+    a.src[t] = d_src[t];
+    a.dst[t] = d_dst[t];
+  }
+  const int Ho = H + top + bottom, Wo = W + left + right;
+  const long long items = planes * Ho * ((Wo + 3) / 4) * count;
+  const long long blocks = (items + 255) / 256;
+  hipLaunchKernelGGL(replicate_pad_kernel, dim3((unsigned)(blocks < 16384 ? blocks : 16384)), dim3(256), 0,
+                     static_cast<hipStream_t>(stream), a, count, planes, H, W, Ho, Wo, top, left);
   return launch_status();
 }
 

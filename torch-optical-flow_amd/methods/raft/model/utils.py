@@ -24,6 +24,12 @@ class InputPadder:
             self._pad = [pad_wd // 2, pad_wd - pad_wd // 2, 0, pad_ht]
 
     def pad(self, *inputs: Tensor) -> List[Tensor]:
+        # GPU fp32 frames (the inference inputs): every frame in one native launch (oflow_replicate_pad_f32, a copy,
+        # bit-exact); anything else (CPU, autograd, other dtypes) through F.pad as the reference
+        if (1 <= len(inputs) <= 4 and all(isinstance(x, Tensor) and x.is_cuda and x.dtype == torch.float32
+                                          and x.dim() >= 2 and x.shape == inputs[0].shape for x in inputs)
+                and not (torch.is_grad_enabled() and any(x.requires_grad for x in inputs))):
+            return _native.replicate_pad(inputs, self._pad)
         return [F.pad(x, self._pad, mode="replicate") for x in inputs]
 
     def unpad(self, x: Tensor) -> Tensor:

@@ -70,6 +70,7 @@ SYMBOLS = (
     "oflow_conv_s32_ex3",
     "oflow_conv_s32_ex4",
     "oflow_normalize_images_f32",
+    "oflow_replicate_pad_f32",
     "oflow_corr_fmap_grad_f32",
     "oflow_grid_warp_backward_f32",
     "oflow_grid_sample_backward_f32",
@@ -204,6 +205,8 @@ def load() -> ctypes.CDLL:
     lib.oflow_conv_s32_ex4.restype = I
     lib.oflow_normalize_images_f32.restype = I
     lib.oflow_normalize_images_f32.argtypes = [P, P, L, P, P, P]
+    lib.oflow_replicate_pad_f32.restype = I
+    lib.oflow_replicate_pad_f32.argtypes = [P, P, I, L, I, I, I, I, I, I, P]
     lib.oflow_conv_s32_ex4.argtypes = list(lib.oflow_conv_s32_ex3.argtypes[:-1]) + [P, P]
     lib.oflow_corr_lookup_backward_f32.restype = I
     lib.oflow_corr_lookup_backward_f32.argtypes = [P, P, I, I, I, I, PP, IP, IP, I, P]
@@ -1110,6 +1113,25 @@ def normalize_images(image0: torch.Tensor, image1: torch.Tensor):
         _check(load().oflow_normalize_images_f32(x0.data_ptr(), x1.data_ptr(), n, y0.data_ptr(), y1.data_ptr(),
                                                  _stream(x0.device)), what)
     return y0, y1
+
+
+def replicate_pad(inputs, pad):
+    """F.pad(x, pad, mode="replicate") (pad = [left, right, top, bottom]) of 1..4 same-shape fp32 GPU tensors of >= 2
+    dims in one launch (oflow_replicate_pad_f32; a copy, bit-exact). Returns new contiguous tensors."""
+    what = "replicate_pad"
+    xs = [_gpu_f32(x, "input", what).contiguous() for x in inputs]  # (strided inputs: copied first)
+    if not 1 <= len(xs) <= 4 or any(x.shape != xs[0].shape or x.device != xs[0].device for x in xs) or xs[0].dim() < 2:
+        raise RuntimeError(f"{what}: 1..4 tensors of one shape (>= 2 dims) on one device")
+    left, right, top, bottom = (int(v) for v in pad)
+    *lead, h, w = xs[0].shape
+    outs = [torch.empty((*lead, h + top + bottom, w + left + right), device=xs[0].device, dtype=torch.float32) for _ in xs]
+    planes = xs[0].numel() // (h * w)
+    src = (ctypes.c_void_p * len(xs))(*[x.data_ptr() for x in xs])
+    dst = (ctypes.c_void_p * len(xs))(*[o.data_ptr() for o in outs])
+    with torch.cuda.device(xs[0].device):
+        _check(load().oflow_replicate_pad_f32(src, dst, len(xs), planes, h, w, top, bottom, left, right,
+                                              _stream(xs[0].device)), what)
+    return outs
 
 
 def flow_prep(coords: torch.Tensor, patches: torch.Tensor, flow0=None, flow1=None) -> None:
