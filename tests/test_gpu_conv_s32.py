@@ -245,6 +245,27 @@ def test_pack_s32_and_flow_prep():
         assert float((N.s32_to_f32(t)[:, 382:] - flow).abs().max()) <= 1e-6 * float(flow.abs().max())
 
 
+@pytest.mark.parametrize("c,dst", [(100, 8), (37, 0), (256, 0), (8, 24)])
+def test_pack_s32_ragged_channels(c, dst):
+    """pack_s32 with channel counts that end mid-group / mid-octet and destinations that start mid-group: every
+    destination value against the act'd source (hi + lo within fp32 rounding), the zero fill of the last octet, the
+    neighbouring channels untouched, and the fp32 NHWC copy exact."""
+    g = torch.Generator().manual_seed(c + dst)
+    b, h, w = 2, 13, 37
+    x = torch.randn(b, c, h, w, generator=g).to(DEV)
+    groups = (dst + ((c + 7) // 8) * 8 + 31) // 32 + 1
+    y = N.s32_from_f32(torch.full((b, groups * 32, h, w), 9.0, device=DEV))
+    f = torch.empty(b * h * w, c, device=DEV)
+    N.pack_s32(x, "relu", N.S32Slice(y), nhwc=f, dst_channel=dst)
+    got = N.s32_to_f32(y).double()
+    ref = torch.relu(x).double()
+    assert float((got[:, dst : dst + c] - ref).abs().max()) <= 2.0 ** -21 * float(ref.abs().max())
+    end = dst + ((c + 7) // 8) * 8
+    assert bool((got[:, dst + c : end] == 0).all())
+    assert bool((got[:, :dst] == 9.0).all()) and bool((got[:, end:] == 9.0).all())
+    assert torch.equal(f.view(b, h, w, c).permute(0, 3, 1, 2), torch.relu(x))
+
+
 @pytest.mark.parametrize("b,h,w", [(2, 11, 29), (4, 55, 128), (1, 47, 156), (3, 5, 3)])
 def test_flow_prep_tiled_equals_per_thread(b, h, w):
     """The LDS-tiled flow_prep (default) against the per-thread form (experiment hook): patch matrix and the GRU inputs'

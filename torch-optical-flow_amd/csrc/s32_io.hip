@@ -35,35 +35,41 @@ __device__ __forceinline__ void put8(uint8_t* line, const float* v) {
   *reinterpret_cast<half8*>(line + 64) = lo;
 }
 
-// one thread = one pixel x 8 channels; consecutive threads = consecutive pixels (coalesced NCHW reads). Source channel
-// c goes to destination channel yc0 + c (yc0 % 8 == 0); the chunk's channels beyond C are written as zeros.
+// one thread = one pixel x 32 channels (4 octets); consecutive threads = consecutive pixels (coalesced NCHW reads).
+// Source channel c goes to destination channel yc0 + c (yc0 % 8 == 0); an octet's channels beyond C are written as
+// zeros. A thread writes its 4 octets back to back (with yc0 % 32 == 0: the whole 128-B S32 line of the group; one
+// thread per octet wrote 16-B pieces of each line at far-apart times: 49 us per 4-pair launch in the step).
 __global__ __launch_bounds__(256) void pack_s32_kernel(const float* __restrict__ x, long long xbs, int C, int B, int HW,
                                                        int act, int yc0, uint8_t* y0, long long y0ps, uint8_t* y1,
                                                        long long y1ps, float* f, int fcs) {
   // 32-bit indexing (the host checks P * C8 < 2^31): 64-bit divisions dominated these memory-bound kernels
   const int P = B * HW;
-  const int C8 = (C + 7) / 8;
+  const int C32 = (C + 31) / 32;
   const int item = blockIdx.x * blockDim.x + threadIdx.x;
-  if (item >= P * C8) return;
-  const int c8 = item / P;
-  const long long p = item - c8 * P;
+  if (item >= P * C32) return;
+  const int c32 = item / P;
+  const long long p = item - c32 * P;
   const int b = static_cast<int>(p) / HW;
   const int pix = static_cast<int>(p) - b * HW;
-  const int c0 = c8 * 8;
-  float v[8];
 #pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    const int c = c0 + j;
-    v[j] = c < C ? act_fn(x[b * xbs + (long long)c * HW + pix], act) : 0.f;
-  }
-  const int cd = yc0 + c0;  // destination channel (multiple of 8)
-  const long long off = (long long)(cd >> 5) * 128 + ((cd & 31) >> 3) * 16;
-  put8(y0 + p * y0ps + off, v);
-  if (y1) put8(y1 + p * y1ps + off, v);
-  if (f) {
+  for (int o = 0; o < 4; ++o) {
+    const int c0 = c32 * 32 + o * 8;
+    if (c0 >= C) break;
+    float v[8];
 #pragma unroll
-    for (int j = 0; j < 8; ++j)
-      if (c0 + j < C) f[p * fcs + c0 + j] = v[j];
+    for (int j = 0; j < 8; ++j) {
+      const int c = c0 + j;
+      v[j] = c < C ? act_fn(x[b * xbs + (long long)c * HW + pix], act) : 0.f;
+    }
+    const int cd = yc0 + c0;  // destination channel (multiple of 8)
+    const long long off = (long long)(cd >> 5) * 128 + ((cd & 31) >> 3) * 16;
+    put8(y0 + p * y0ps + off, v);
+    if (y1) put8(y1 + p * y1ps + off, v);
+    if (f) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        if (c0 + j < C) f[p * fcs + c0 + j] = v[j];
+    }
   }
 }
 
@@ -404,7 +410,7 @@ extern "C" int oflow_pack_s32_f32(const float* d_x, long long x_batch_stride, in
   if (activation < 0 || activation > 3) return OFLOW_E_MODE;
   if ((y0_pixel_stride & 127) || ((uintptr_t)d_y0 & 15) || (d_y1 && ((y1_pixel_stride & 127) || ((uintptr_t)d_y1 & 15))))
     return OFLOW_E_ALIGN;
-  const long long items = (long long)B * H * W * ((C + 7) / 8);
+  const long long items = (long long)B * H * W * ((C + 31) / 32);
   if ((items + 255) / 256 * 256 >= (1ll << 31)) return OFLOW_E_SHAPE;  // 32-bit indexing over the rounded-up grid
   hipLaunchKernelGGL(pack_s32_kernel, dim3((unsigned)((items + 255) / 256)), dim3(256), 0, static_cast<hipStream_t>(stream),
                      d_x, x_batch_stride, C, B, H * W, activation, dst_channel, static_cast<uint8_t*>(d_y0), y0_pixel_stride,
