@@ -103,7 +103,6 @@ class RAFT(nn.Module):
         self.encoder_impl = "split"
         self.encoder_streams = True  # cnet beside fnet + the corr pyramid (inference, split encoders)
         self.fnet_streams = True  # with encoder_streams: fnet's image0 and image1 halves on two streams
-        self.cnet_after_fnet = False  # with encoder_streams: cnet after fnet, beside the pyramid (experiment)
         # split update loop over >= 2 pairs (CorrBlock): the pairs' two halves run on two streams so that one half's
         # convolutions fill the CUs the other half's leave idle at a wave tail. pair_lookup "joined": one full-batch
         # lookup per iteration on the main stream (both halves joined around it); "lane": each half looks up its own.
@@ -331,10 +330,7 @@ class RAFT(nn.Module):
             else:
                 patches = None if sfi else fnet.stem_patches(torch.cat([image0, image1], dim=0))
             cpatches = None if patches is None else patches[:nb]
-            # cnet_after_fnet: cnet starts when fnet is done and runs beside the (store-bound) pyramid instead of
-            # beside fnet's halves
-            cnet_late = side is not None and self.cnet_after_fnet and block is CorrBlock and self.split_corr
-            if side is not None and not cnet_late:
+            if side is not None:
                 side.wait_stream(main)
                 with torch.cuda.stream(side):
                     cnet_out = cnet(image0, patches=cpatches, stem_from_image=sfi)
@@ -345,10 +341,6 @@ class RAFT(nn.Module):
                     main.wait_stream(side2)
                 else:
                     f1s, f2s = fnet([image0, image1], patches=patches, split_out=True, stem_from_image=sfi)
-                if cnet_late:
-                    side.wait_stream(main)
-                    with torch.cuda.stream(side):
-                        cnet_out = cnet(image0, patches=cpatches, stem_from_image=sfi)
                 corr_fn = CorrBlock.from_split_features(f1s, f2s, radius=self.hparams.corr_radius)
             else:
                 fmap1, fmap2 = fnet([image0, image1], patches=patches, stem_from_image=sfi)
