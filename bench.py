@@ -367,6 +367,10 @@ def main() -> int:
                          "encoders run beside step i's update loop (pairs are independent; every step's flows are its own)")
     ap.add_argument("--no-step-flops", action="store_true",
                     help="skip the untimed flop-counting forward (roofline.step), e.g. under a kernel-trace profiler")
+    ap.add_argument("--no-comm-overlap", action="store_true",
+                    help="N > 1: run scatter -> forward -> gathers back to back per step (default: the scatter of step "
+                         "i+1 and the gathers of step i overlap step i's / i+1's forward, model/pair_sharding.py "
+                         "infer_sharded_pipelined)")
     ap.add_argument("--range-guard", default=None, choices=["sync", "deferred", "off"],
                     help="RAFT.range_guard (default: the model's, 'deferred': checked after the timed region)")
     args = ap.parse_args()
@@ -383,7 +387,7 @@ def main() -> int:
         dist.init_process_group("nccl", device_id=dev)
 
     from model import RAFT, InputPadder, synthetic
-    from model.pair_sharding import infer_sharded
+    from model.pair_sharding import infer_sharded, infer_sharded_pipelined
     from optical_flow import _native
 
     ppg, h, w, iters, pmode, alt = WORKLOADS[args.workload]
@@ -463,9 +467,21 @@ def main() -> int:
         with torch.cuda.stream(streams[i % len(streams)]):
             return step()
 
+    # N > 1: communication overlapped with the forwards (scatter of step i+1 / gathers of step i on the RCCL stream)
+    pipelined = world > 1 and args.workload != "corr" and not args.no_comm_overlap
+
+    def run_steps(n):
+        out = None
+        if pipelined:
+            for out in infer_sharded_pipelined(fwd, ((img0, img1) for _ in range(n)), dev, shard_shape, flow_shapes):
+                pass
+            return out
+        for i in range(n):
+            out = issue(i)
+        return out
+
     with torch.inference_mode():
-        for i in range(max(args.warmup, len(streams))):
-            issue(i)
+        run_steps(max(args.warmup, 1 if pipelined else len(streams)))
         torch.cuda.synchronize(dev)
         # graph replays launch no Python, so no per-kernel events (the roofline comes from an eager run)
         rec = ({"*": True} if args.conv_events else {}) if not (args.no_events or args.graph) else None
@@ -474,8 +490,7 @@ def main() -> int:
             dist.barrier()
         torch.cuda.synchronize(dev)
         t0 = time.perf_counter()
-        for i in range(args.steps):
-            out = issue(i)
+        out = run_steps(args.steps)
         torch.cuda.synchronize(dev)
         if world > 1:
             dist.barrier()
@@ -540,7 +555,9 @@ def main() -> int:
             "global_batch": global_batch,
             "iters": iters,
             "padded": f"{dims[0][0] * 8}x{dims[0][1] * 8}",
-            "parallelism": f"pairs sharded over {world} GPU(s)" + (", RCCL scatter/gather" if world > 1 else ""),
+            "parallelism": f"pairs sharded over {world} GPU(s)"
+            + ((", RCCL scatter/gather overlapped with the forwards" if pipelined else ", RCCL scatter/gather")
+               if world > 1 else ""),
             "conv_benchmark": not args.no_conv_benchmark,
             "update_impl": args.update_impl,
             "hip_graph": bool(args.graph),

@@ -218,6 +218,13 @@ int oflow_replicate_pad_f32(const float* const* d_src, float* const* d_dst, int 
  * fp16 (|x| >= 65520 or inf); it is never cleared by the library. Synchronous (a copy to each kernel module's symbol). */
 int oflow_set_range_flag(unsigned int* d_flag);
 
+/* oflow_range_flag_exchange: *d_out = the range flag's value, and the flag cleared, in one device atomic exchange on
+ * `stream` (enqueued after a forward's kernels: that forward's snapshot; an overflow set concurrently by a forward on
+ * another stream lands in this snapshot or the next one, never lost). d_flag: the pointer given to
+ * oflow_set_range_flag; d_out: one unsigned int of device memory. Replaces nothing in the reference (the split-fp16
+ * range guard of RAFT.forward, methods/raft/model/raft.py:87-147, is this build's addition). */
+int oflow_range_flag_exchange(unsigned int* d_flag, unsigned int* d_out, void* stream);
+
 int oflow_flow_head2_s32(const void* d_x, long long x_pixel_stride, int in_groups, const float* d_weight,
                          const float* d_bias, int B, int H, int W, float* d_coords, void* stream);
 /* oflow_corr_lookup_tiled_nhwc_f32: the tiled lookup as fp32 NHWC rows [B*H*W][row_floats] (d_out 16-B aligned) in the
@@ -304,8 +311,11 @@ int oflow_conv_s32_ex3(const void* d_x, long long x_pixel_stride, int in_groups,
                        long long addend_pixel_stride, void* stream);
 /* oflow_conv_s32_ex4: oflow_conv_s32_ex3 plus d_wfrag, an optional fragment-major copy of d_wpack (same bytes, reordered
  * [group][tap][n/32][slice][hi|lo][k half][row][8] so that one wave's 32x16 MFMA B fragment is 1 KB contiguous and is
- * loaded straight into registers, skipping the LDS staging of B). Used for block_n 128 convolutions with more than one
- * tap; other shapes ignore it. NULL = ex3. */
+ * loaded straight into registers, skipping the LDS staging of B). Used, on S32 input without instance-norm partials
+ * outside the small-grid tiles, by every multi-tap convolution with block_n 128 and by 3x3 convolutions with block_n 64
+ * or 32; other shapes ignore it. The block_n 64 / 32 register-direct variants measured slower in the RAFT step
+ * (DESIGN.md §4, r04): pass NULL for them unless comparing (the Python layer passes d_wfrag for them only under
+ * OFLOW_CONV_BREG64 / OFLOW_CONV_BREG32). NULL = ex3. */
 int oflow_conv_s32_ex4(const void* d_x, long long x_pixel_stride, int in_groups, const void* d_wpack, int n_pad,
                        const float* d_wscale, const float* d_bias, int N, int B, int H, int W, int kh, int kw,
                        int block_n, int epilogue, int activation, float out_scale, void* d_y0, long long y0_pixel_stride,

@@ -196,6 +196,28 @@ def test_predict_pipeline_writes_reference_files(tmp_path):
         assert np.abs(png.astype(int) - want.astype(int)).max() <= 1
 
 
+def test_predict_writes_nothing_for_an_overflowing_pair(tmp_path):
+    """predict.py's writer checks each pair's own split-fp16 range snapshot (RAFT.last_range_snapshot) before writing:
+    with convc1 weights scaled so that every forward overflows, the run raises and leaves no .flo / .png behind."""
+    import predict
+    from PIL import Image
+    from model import RAFT
+
+    src = tmp_path / "frames"
+    src.mkdir()
+    for k in range(2):
+        img, _ = synthetic.synthetic_pair(1, 128, 160, seed=30 + k)
+        Image.fromarray(img[0].permute(1, 2, 0).clamp(0, 255).to(torch.uint8).numpy(), "RGB").save(src / f"f{k}.png")
+    model = RAFT()
+    sd = synthetic.synthetic_state_dict(model.state_dict())
+    sd["update_block.encoder.convc1.weight"] = sd["update_block.encoder.convc1.weight"] * 1e6
+    torch.save(sd, tmp_path / "bad.pth")
+    with pytest.raises(RuntimeError, match="fp16 range"):
+        predict.main(str(src), str(tmp_path / "out"), checkpoint=str(tmp_path / "bad.pth"), iters=2, eval_mode=True,
+                     num_workers=0)
+    assert not list((tmp_path / "out").glob("*.flo")) and not list((tmp_path / "out").glob("*.png"))
+
+
 def test_model_built_under_inference_mode(golden):
     # predict.py:39 builds the model inside @torch.inference_mode(): its weights are inference tensors (no
     # version counter), which the packed-weight caches must accept

@@ -348,8 +348,8 @@ def test_graphed_forward_equals_eager():
 
 def test_graphed_multi_pair_forward_equals_eager_two_lanes():
     """GraphedRAFT on a multi-pair batch (3 pairs, above the flow-head threshold: the conv flow head) is captured with
-    one pair lane (the two-lane capture crashes in capture_end) and replays the eager two-lane forward's flows bit for
-    bit; the model's pair_lanes setting is restored after the capture."""
+    two pair lanes (without the lanes' side streams, whose nested fork crashes hipStreamEndCapture) and replays the
+    eager two-lane forward's flows bit for bit; the model's settings are restored after the capture."""
     from model.graph import GraphedRAFT
 
     model = _model(RAFT)
@@ -359,7 +359,7 @@ def test_graphed_multi_pair_forward_equals_eager_two_lanes():
     p0, p1 = (x.to(DEV) for x in padder.pad(a0, a1))
     with torch.inference_mode():
         g = GraphedRAFT(model, p0, p1, iters=6)
-        assert model.pair_lanes == 2
+        assert model.pair_lanes == 2 and getattr(model.update_block, "split_streams", True)
         lo_e, up_e = model(p0, p1, iters=6, test_mode=True)
         lo_g, up_g = g(p0, p1)
         assert torch.equal(lo_g, lo_e) and torch.equal(up_g, up_e)
@@ -419,6 +419,25 @@ def test_range_guard_deferred_mode():
         g(p0 * 1e6, p1 * 1e6)
         with pytest.raises(RuntimeError, match="fp16 range"):
             bad.check_range(DEV)
+
+
+def test_range_snapshot_per_forward():
+    """Each GPU inference forward's own range status (RAFT.last_range_snapshot, oflow_range_flag_exchange: the flag read
+    and cleared in one device-side exchange after the forward's kernels): an overflowing forward followed by a valid one
+    -- neither waited on -- report True and False respectively, and the deferred check then raises once."""
+    img0, img1 = synthetic.synthetic_pair(1, 128, 160, seed=6)
+    p0, p1 = img0.to(DEV), img1.to(DEV)
+    m = _model(RAFT)
+    with torch.inference_mode():
+        m(p0 * 1e6, p1 * 1e6, iters=2, test_mode=True)
+        bad = m.last_range_snapshot
+        m(p0, p1, iters=2, test_mode=True)
+        good = m.last_range_snapshot
+        assert bad is not good
+        assert bad.overflowed() and not good.overflowed()
+        with pytest.raises(RuntimeError, match="fp16 range"):
+            m.check_range()
+        m.check_range(DEV)  # nothing left set
 
 
 def test_forwards_in_flight_on_two_streams_equal_sequential():

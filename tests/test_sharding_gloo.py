@@ -161,3 +161,48 @@ def test_scatter_refuses_a_shape_that_disagrees_with_the_batch(world):
     assert res[0] == (0, ("ValueError", "ok", "ValueError", "ValueError"))
     for r in res[1:]:
         assert r[1] == ("ValueError", "ok", "nan", "none"), r
+
+
+def _pipeline_worker(rank, world, port, batch, steps, q):
+    """infer_sharded_pipelined (scatter of step i+1 and gathers of step i in flight around step i's forward) vs
+    infer_sharded step by step, on distinct batches per step."""
+    from model.pair_sharding import infer_sharded_pipelined
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        g = torch.Generator().manual_seed(1)
+        data = [(torch.rand(batch, 3, 16, 24, generator=g) * 255, torch.rand(batch, 3, 16, 24, generator=g) * 255)
+                for _ in range(steps)]
+        cpu = torch.device("cpu")
+        shape = (batch, 3, 16, 24)
+        flow_shapes = ((2, 2, 3), (2, 16, 24))
+        seq = [infer_sharded(_fake_forward, *(d if rank == 0 else (None, None)), cpu, shape=shape, flow_shapes=flow_shapes)
+               for d in data]
+        calls = []
+
+        def fwd(a, b):
+            calls.append(a.shape[0])
+            return _fake_forward(a, b)
+
+        batches = (d if rank == 0 else (None, None) for d in data)
+        pipe = list(infer_sharded_pipelined(fwd, batches, cpu, shape=shape, flow_shapes=flow_shapes))
+        ok = len(pipe) == steps
+        for (lo, up), (rl, ru) in zip(pipe, seq):
+            if rank == 0:
+                ok = ok and torch.equal(lo, rl) and torch.equal(up, ru)
+            else:
+                ok = ok and lo is None and up is None and rl is None and ru is None
+        st, sp = shard_bounds(batch, world, rank)
+        ok = ok and calls == ([sp - st] * steps if sp > st else [])
+        q.put((rank, ok))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,batch,steps", [(2, 8, 3), (2, 5, 1), (3, 2, 2)])
+def test_pipelined_steps_equal_sequential_gloo(world, batch, steps):
+    """The overlapped step driver bench.py --gpus N uses returns every step's flows exactly as the sequential
+    scatter -> forward -> gather does, including a ragged batch, one step, and a rank without pairs."""
+    res = _run(_pipeline_worker, world, batch, steps)
+    assert all(r[1] for r in res), res

@@ -4,9 +4,14 @@ dispatch of its counters and the derived matrix-core figures.
     python tools/pmc_mfma.py <pass1 counter_collection.csv> <pass2 counter_collection.csv> [--json out.json]
 
 Derived (MI355X_MICROARCH.md: SQ_VALU_MFMA_BUSY_CYCLES counts SIMD cycles, 32 per 32x32x16 f16 MFMA; SQ_WAVE_CYCLES /
-SQ_WAIT_* / SQ_ACTIVE_INST_* count quad-cycles; GRBM_GUI_ACTIVE is summed over the 8 XCDs):
-  clock_ghz     = GRBM_GUI_ACTIVE / 8 / duration
-  mfma_util     = SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE / 8 * 1024 SIMDs)   (fraction of SIMD-cycles busy on MFMA)
+SQ_WAIT_* / SQ_ACTIVE_INST_* count quad-cycles; GRBM_GUI_ACTIVE is summed over the 8 XCDs, SQ_BUSY_CYCLES over the 32
+shader engines):
+  clock_ghz_grbm = GRBM_GUI_ACTIVE / 8 / duration: reads high on dispatches shorter than ~0.3 ms (the guide's DVFS
+                   note; r04 saw 2.9-3.6 GHz for short kernels, above the chip's 2.4 GHz)
+  clock_ghz      = the dispatch's own clock: SQ_BUSY_CYCLES / 32 / duration when that lies in [1.0, 2.4] GHz, else
+                   min(clock_ghz_grbm, 2.4); `clock_source` says which
+  mfma_util      = SQ_VALU_MFMA_BUSY_CYCLES / (duration * clock_ghz * 1024 SIMDs)   (fraction of SIMD-cycles busy on MFMA)
+  mfma_util_2p4  = the same at the nominal 2.4 GHz (a lower bound on the fraction)
   busy_per_mfma = SQ_VALU_MFMA_BUSY_CYCLES / SQ_INSTS_MFMA   (32 expected for 32x32x16 f16)
   wait_any / wait_inst / active = SQ_WAIT_ANY / SQ_WAIT_INST_ANY / SQ_ACTIVE_INST_ANY over SQ_WAVE_CYCLES
   lds_conflict  = SQ_LDS_BANK_CONFLICT / SQ_LDS_IDX_ACTIVE
@@ -50,10 +55,22 @@ def main():
         med = {c: statistics.median(v) for c, v in cs.items()}
         row = {"kernel": k, "grid": g, "dispatches": len(cs["_dur_ns"]), "us": round(med["_dur_ns"] / 1e3, 2)}
         gui = med.get("GRBM_GUI_ACTIVE")
+        dur = med["_dur_ns"]
+        clk, src = None, None
+        if med.get("SQ_BUSY_CYCLES"):
+            c = med["SQ_BUSY_CYCLES"] / 32 / dur
+            row["clock_ghz_sq_busy"] = round(c, 3)
+            if 1.0 <= c <= 2.4:
+                clk, src = c, "SQ_BUSY_CYCLES"
         if gui:
-            row["clock_ghz"] = round(gui / 8 / med["_dur_ns"], 3)
+            row["clock_ghz_grbm"] = round(gui / 8 / dur, 3)
+            if clk is None:
+                clk, src = min(gui / 8 / dur, 2.4), "GRBM_GUI_ACTIVE (capped at 2.4 GHz)"
+        if clk is not None:
+            row["clock_ghz"], row["clock_source"] = round(clk, 3), src
             if "SQ_VALU_MFMA_BUSY_CYCLES" in med:
-                row["mfma_util"] = round(med["SQ_VALU_MFMA_BUSY_CYCLES"] / (gui / 8 * 1024), 4)
+                row["mfma_util"] = round(med["SQ_VALU_MFMA_BUSY_CYCLES"] / (dur * clk * 1024), 4)
+                row["mfma_util_2p4"] = round(med["SQ_VALU_MFMA_BUSY_CYCLES"] / (dur * 2.4 * 1024), 4)
         if med.get("SQ_INSTS_MFMA"):
             row["mfma_insts"] = med["SQ_INSTS_MFMA"]
             if "SQ_VALU_MFMA_BUSY_CYCLES" in med:

@@ -13,6 +13,18 @@ extern "C" int oflow_set_range_flag(unsigned int* d_flag) {
   return st;  // OFLOW_OK or a HIP error code (positive)
 }
 
+namespace {
+__global__ void range_flag_exchange_kernel(unsigned int* flag, unsigned int* out) {
+  if (threadIdx.x == 0) *out = atomicExch(flag, 0u);
+}
+}  // namespace
+
+extern "C" int oflow_range_flag_exchange(unsigned int* d_flag, unsigned int* d_out, void* stream) {
+  if (!d_flag || !d_out) return OFLOW_E_NULL;
+  hipLaunchKernelGGL(range_flag_exchange_kernel, dim3(1), dim3(64), 0, static_cast<hipStream_t>(stream), d_flag, d_out);
+  return oflow::launch_status();
+}
+
 extern "C" const char* oflow_status_string(int status) {
   switch (status) {
     case OFLOW_OK: return "ok";

@@ -17,6 +17,14 @@ from typing import Tuple
 import torch
 from torch import Tensor
 
+from . import update as _update
+
+# A multi-pair forward is captured with its pair lanes (RAFT.pair_lanes) but without the per-lane side streams of the
+# update block (update_block.split_streams): a side stream forked from a lane stream -- itself forked from the capture
+# stream -- makes hipStreamEndCapture segfault (profiles/r04/s12_graph8.log, profiles/r05/s1_probe_flag.log; the same
+# capture without those nested forks replays bit-identically, 18.57 ms vs 18.91 ms eager for 8 Sintel pairs:
+# profiles/r05/s2_probe_noside.log). The model's settings are restored after the capture. None: capture as configured.
+CAPTURE_LANE_SIDE_STREAMS = False
 
 class GraphedRAFT:
     """``model(image0, image1, iters, test_mode=True)`` captured for the shapes of ``image0`` / ``image1``.
@@ -39,17 +47,14 @@ class GraphedRAFT:
         self.image0 = image0.detach().clone()
         self.image1 = image1.detach().clone()
         dev = image0.device
-        # multi-pair batches are captured with one pair lane: capturing the two-lane update loop (each lane with its
-        # own side stream) segfaults inside capture_end (profiles/r04/s12_graph8.log); one lane captures and replays
-        # bit-identically to the eager forward (tools/exp/graph_probe.py, 8 pairs: replay 19.72 ms vs eager two-lane
-        # 19.62 ms, profiles/r04/s32_graph8l1.log). The model's own setting is restored after the capture.
-        lanes = getattr(model, "pair_lanes", 1)
-        if image0.shape[0] > 1 and lanes > 1:
-            model.pair_lanes = 1
+        blk = model.update_block
+        side = getattr(blk, "split_streams", True)
+        if CAPTURE_LANE_SIDE_STREAMS is not None and image0.shape[0] > 1 and getattr(model, "pair_lanes", 1) > 1:
+            blk.split_streams = CAPTURE_LANE_SIDE_STREAMS
         try:
             self._capture(model, iters, warmup, dev)
         finally:
-            model.pair_lanes = lanes
+            blk.split_streams = side
 
     def _capture(self, model, iters: int, warmup: int, dev) -> None:
         with torch.inference_mode():
@@ -63,8 +68,14 @@ class GraphedRAFT:
             self.graph = torch.cuda.CUDAGraph()
             # captured on the warm-up stream: the side / lane streams the forward forks to (keyed by their owner
             # stream, model/update.py _side_stream) are the ones the warm-up created
-            with torch.cuda.graph(self.graph, stream=side):
-                self.flow_low, self.flow_up = model(self.image0, self.image1, iters=iters, test_mode=True)
+            # capture_active(): the pair lanes' streams join the capture through event waits and on ROCm do not report
+            # themselves as capturing; the weight caches must not wait on their (pre-capture) events from any of them
+            _update._CAPTURE_DEPTH[0] += 1
+            try:
+                with torch.cuda.graph(self.graph, stream=side):
+                    self.flow_low, self.flow_up = model(self.image0, self.image1, iters=iters, test_mode=True)
+            finally:
+                _update._CAPTURE_DEPTH[0] -= 1
 
     def __call__(self, image0: Tensor, image1: Tensor) -> Tuple[Tensor, Tensor]:
         if image0.shape != self.image0.shape or image1.shape != self.image1.shape:

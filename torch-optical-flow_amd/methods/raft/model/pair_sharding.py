@@ -11,7 +11,7 @@ to equal chunks for the collective and trimmed on both sides; a rank with no pai
 """
 from __future__ import annotations
 
-from typing import Callable, Optional, Sequence, Tuple
+from typing import Callable, Iterable, Iterator, Optional, Sequence, Tuple
 
 import torch
 import torch.distributed as dist
@@ -42,7 +42,14 @@ def _meta(t: Optional[Tensor], src: int, group, device: torch.device) -> Sequenc
     return v[1 : 1 + v[0]]
 
 
-_VALIDATED = set()  # (shape, group, src) checked collectively once per process (see scatter_pairs)
+_VALIDATED = set()  # (shape, process group object, world size, src) checked collectively (see scatter_pairs)
+
+
+def _group_key(group):
+    """The process group itself (the key holds a reference, so a destroyed and re-created group -- a new object -- is
+    validated again) with its size."""
+    pg = group if group is not None else dist.distributed_c10d._get_default_group()
+    return pg, dist.get_world_size(group)
 
 
 def _check_shape_collectively(shape, image0, image1, src: int, group, device: torch.device) -> None:
@@ -50,7 +57,7 @@ def _check_shape_collectively(shape, image0, image1, src: int, group, device: to
     global ``shape`` and every rank raises the same ValueError on a mismatch (one 8-byte broadcast + one host sync
     per run, not per step)."""
     world, rank = _world(group)
-    key = (tuple(int(v) for v in shape), id(group) if group is not None else None, src)
+    key = (tuple(int(v) for v in shape), *_group_key(group), src)
     if key in _VALIDATED:
         return
     ok = torch.zeros(1, dtype=torch.int64, device=device)
@@ -63,7 +70,11 @@ def _check_shape_collectively(shape, image0, image1, src: int, group, device: to
     _VALIDATED.add(key)
 
 
-def _scatter(image0, image1, device, src, group, shape):
+def _src_rank(group, src):
+    return dist.get_global_rank(group, src) if group is not None else src
+
+
+def _scatter(image0, image1, device, src, group, shape, async_op: bool = False):
     """The scatter; returns (shard0, shard1, error). A source batch that disagrees with a caller-given ``shape`` after
     the one-time collective check (the source's batch changed shape mid-run) still completes the collective with
     NaN pieces of the agreed size, so no peer blocks; the source gets the ValueError back to raise afterwards."""
@@ -77,7 +88,7 @@ def _scatter(image0, image1, device, src, group, shape):
     b, rest = shape[0], shape[1:]
     chunk = -(-b // world)
     start, stop = shard_bounds(b, world, rank)
-    outs = []
+    outs, works = [], []
     for img in (image0, image1):
         recv = torch.empty([chunk] + rest, dtype=torch.float32, device=device)
         scatter_list = None
@@ -93,8 +104,11 @@ def _scatter(image0, image1, device, src, group, shape):
                     if s1 - s0 < chunk:
                         piece = torch.cat([piece, piece.new_zeros([chunk - (s1 - s0)] + rest)], dim=0)
                     scatter_list.append(piece.contiguous())
-        dist.scatter(recv, scatter_list, src=dist.get_global_rank(group, src) if group is not None else src, group=group)
+        w = dist.scatter(recv, scatter_list, src=_src_rank(group, src), group=group, async_op=async_op)
+        works.append(w)
         outs.append(recv[: stop - start])
+    if async_op:
+        return outs[0], outs[1], err, works
     return outs[0], outs[1], err
 
 
@@ -117,8 +131,28 @@ def scatter_pairs(
     return s0, s1
 
 
-def gather_flows(flow: Tensor, global_batch: int, dst: int = 0, group=None) -> Optional[Tensor]:
-    """Gather every rank's (b_r, ...) flow shard to rank ``dst``; returns the (B, ...) batch there, else None."""
+class _PendingGather:
+    """An issued (async) gather of flow shards to ``dst``: ``result()`` waits for it and returns the (B, ...) batch on
+    ``dst``, None elsewhere."""
+
+    __slots__ = ("work", "gather_list", "global_batch", "world", "is_dst")
+
+    def __init__(self, work, gather_list, global_batch: int, world: int, is_dst: bool) -> None:
+        self.work, self.gather_list, self.global_batch, self.world, self.is_dst = work, gather_list, global_batch, world, is_dst
+
+    def result(self) -> Optional[Tensor]:
+        if self.work is not None:
+            self.work.wait()  # RCCL: the current stream waits for the collective (no host block); gloo: the host waits
+        if not self.is_dst:
+            return None
+        parts = []
+        for r in range(self.world):
+            s0, s1 = shard_bounds(self.global_batch, self.world, r)
+            parts.append(self.gather_list[r][: s1 - s0])
+        return torch.cat(parts, dim=0)
+
+
+def _gather(flow: Tensor, global_batch: int, dst: int, group, async_op: bool) -> _PendingGather:
     world, rank = _world(group)
     chunk = -(-global_batch // world)
     rest = list(flow.shape[1:])
@@ -127,14 +161,13 @@ def gather_flows(flow: Tensor, global_batch: int, dst: int = 0, group=None) -> O
         send = torch.cat([flow, flow.new_zeros([chunk - flow.shape[0]] + rest)], dim=0)
     send = send.contiguous()
     gather_list = [torch.empty_like(send) for _ in range(world)] if rank == dst else None
-    dist.gather(send, gather_list, dst=dist.get_global_rank(group, dst) if group is not None else dst, group=group)
-    if rank != dst:
-        return None
-    parts = []
-    for r in range(world):
-        s0, s1 = shard_bounds(global_batch, world, r)
-        parts.append(gather_list[r][: s1 - s0])
-    return torch.cat(parts, dim=0)
+    w = dist.gather(send, gather_list, dst=_src_rank(group, dst), group=group, async_op=async_op)
+    return _PendingGather(w, gather_list, global_batch, world, rank == dst)
+
+
+def gather_flows(flow: Tensor, global_batch: int, dst: int = 0, group=None) -> Optional[Tensor]:
+    """Gather every rank's (b_r, ...) flow shard to rank ``dst``; returns the (B, ...) batch there, else None."""
+    return _gather(flow, global_batch, dst, group, async_op=False).result()
 
 
 def infer_sharded(
@@ -172,3 +205,57 @@ def infer_sharded(
     if err is not None:  # every rank has completed the step's collectives
         raise err
     return out
+
+
+def infer_sharded_pipelined(
+    forward: Callable[[Tensor, Tensor], Tuple[Tensor, Tensor]],
+    batches: Iterable[Tuple[Optional[Tensor], Optional[Tensor]]],
+    device: torch.device,
+    shape: Sequence[int],
+    flow_shapes: Tuple[Sequence[int], Sequence[int]],
+    src: int = 0,
+    group=None,
+) -> Iterator[Tuple[Optional[Tensor], Optional[Tensor]]]:
+    """``infer_sharded`` over a stream of pair batches (rank ``src`` yields its (image0, image1) per step, the other
+    ranks yield (None, None) the same number of times) with the communication off the compute stream's critical path:
+    the scatter of step i+1 is issued (async) before step i's forward, so it runs on the RCCL stream while the forward
+    runs, and step i's two gathers are issued right after its forward and overlap step i+1's forward. The compute stream
+    waits for a step's scatter only when that step's forward starts (``work.wait()``: a stream-side wait under RCCL).
+    Yields each step's (flow_low, flow_up) on ``src`` ((None, None) elsewhere) one step late, then the last one: the
+    same flows, in the same order, as ``infer_sharded`` per step (tests/test_sharding_gloo.py). Collectives are issued
+    in the same order on every rank: scatter 0, then per step i: scatter i+1, gathers i. Shapes are fixed for the run
+    (``shape`` global (B, C, H, W), ``flow_shapes`` as in ``infer_sharded``)."""
+    b = int(shape[0])
+    it = iter(batches)
+
+    def scatter(batch):
+        s0, s1, err, works = _scatter(batch[0], batch[1], device, src, group, shape, async_op=True)
+        return s0, s1, err, works
+
+    cur = next(it, None)
+    pend_scatter = scatter(cur) if cur is not None else None
+    prev = None  # (gather low, gather up, err) of the previous step
+    while pend_scatter is not None:
+        s0, s1, err, works = pend_scatter
+        for w in works:
+            if w is not None:
+                w.wait()
+        nxt = next(it, None)
+        pend_scatter = scatter(nxt) if nxt is not None else None  # in flight during this step's forward
+        if s0.shape[0] == 0 or err is not None:
+            low = s0.new_zeros([0] + list(flow_shapes[0]))
+            up = s0.new_zeros([0] + list(flow_shapes[1]))
+        else:
+            low, up = forward(s0, s1)
+        gathers = (_gather(low, b, src, group, async_op=True), _gather(up, b, src, group, async_op=True), err)
+        if prev is not None:
+            out = prev[0].result(), prev[1].result()
+            if prev[2] is not None:
+                raise prev[2]
+            yield out
+        prev = gathers
+    if prev is not None:
+        out = prev[0].result(), prev[1].result()
+        if prev[2] is not None:
+            raise prev[2]
+        yield out

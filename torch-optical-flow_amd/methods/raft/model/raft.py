@@ -32,7 +32,7 @@ from optical_flow import _native
 
 from .corr import AlternateCorrBlock, CorrBlock
 from .extractor import BasicEncoder, SplitEncoder
-from .update import BasicUpdateBlock, FusedUpdate, SplitUpdate, _side_stream
+from .update import BasicUpdateBlock, FusedUpdate, SplitUpdate, _side_stream, capture_active
 from .utils import coords_grid, upflow8
 
 # RAFT.forward's input scaling (raft.py:104-105) through oflow_normalize_images_f32 on GPU inference: one kernel for
@@ -117,13 +117,17 @@ class RAFT(nn.Module):
         # split encoders: the stem convolution builds its 7x7 patch operand from the image tile by tile
         # (OFLOW_IN_IMG7S2) instead of reading a patch matrix written beforehand (fnet's image0 rows shared with cnet)
         self.stem_from_image = True
-        # the split-fp16 range guard (csrc: a sticky device flag set when an operand's hi half overflows fp16).
-        # "deferred" (default): each GPU inference forward snapshots the flag asynchronously (pinned copy + event); a
-        # later forward raises once the GPU is past the overflowing one, and check_range() waits and raises -- no
-        # host sync in the forward. "sync": read at the end of every forward and raise there (one 4-byte D2H copy, a
-        # host sync per forward: -2.5 % on the 8-pair bench step, profiles/r04/s1_bench*.log). "off": never read.
+        # the split-fp16 range guard (csrc: a sticky device flag set when an operand's hi half overflows fp16). After
+        # each GPU inference forward the flag is read and cleared in one device-side exchange on the forward's stream
+        # (``_native.RangeSnapshot``: that forward's own status, copied to pinned memory behind an event).
+        # "deferred" (default): no host sync in the forward; the snapshot is ``last_range_snapshot`` (callers that
+        # consume the output asynchronously check it before using it, as predict.py's writer does), a later forward
+        # raises once the GPU is past an overflowing one, and check_range() waits and raises. "sync": the forward
+        # waits for its snapshot and raises (one host sync per forward: -2.5 % on the 8-pair bench step,
+        # profiles/r04/s1_bench*.log). "off": never read (the flag then stays set until another model reads it).
         self.range_guard = "deferred"
-        self._range_pending = None
+        self._range_pending = []  # deferred snapshots not yet checked, in issue order
+        self.last_range_snapshot = None
         # the split paths cache packed fp16 hi/lo weights keyed by (storage, version); parameters created under
         # torch.inference_mode() have no version counter, so loading new weights in place drops the caches
         for m in (self.fnet, self.cnet, self.update_block):
@@ -192,14 +196,22 @@ class RAFT(nn.Module):
         # the packed weights (built on first use, by kernels on this stream) must exist before the lanes fork: the
         # lanes read them with no later join when the lookup is not joined (fused into convc1, or pair_lookup "lane")
         SplitUpdate._weights(self.update_block)
-        for st in lanes[1:]:
-            st.wait_stream(main)
+        # lane_init_on_main: the lanes' buffers are allocated (and their loop-invariant context terms computed) on the
+        # main stream before the fork, so that no lane allocates from its own stream
+        init_main = getattr(self, "lane_init_on_main", False)
+        if not init_main:
+            for st in lanes[1:]:
+                st.wait_stream(main)
         runners = []
         for i, ((b0, b1), st) in enumerate(zip(cuts, lanes)):
-            with torch.cuda.stream(st):
+            with torch.cuda.stream(main if init_main else st):
                 slot = 0 if i == 0 else 200 + i
                 runners.append(SplitUpdate(self.update_block, cnet_out[b0:b1], hdim, side_slot=slot, fuse_c1=self.lookup_fusion,
-                                           flow_head_pixels=cnet_out.shape[0] * cnet_out.shape[2] * cnet_out.shape[3]))
+                                           flow_head_pixels=cnet_out.shape[0] * cnet_out.shape[2] * cnet_out.shape[3],
+                                           side_owner=st))
+        if init_main:
+            for st in lanes[1:]:
+                st.wait_stream(main)
         joined = self.pair_lookup == "joined" and not runners[0].fusable(corr_fn)
         hw = cnet_out.shape[2] * cnet_out.shape[3]
         if joined:
@@ -234,15 +246,14 @@ class RAFT(nn.Module):
         return outs
 
     def check_range(self, device=None) -> None:
-        """Raise if a split-fp16 operand overflowed in any forward since the last check (waits for the GPU; with
-        ``device`` for every stream of it)."""
-        pend, self._range_pending = self._range_pending, None
-        if pend is not None:
-            pend[1].synchronize()
-            if int(pend[0].item()):
-                _native.range_flag(pend[2]).zero_()
-                raise RuntimeError("RAFT forward: a split-fp16 operand exceeded the fp16 range (|x| >= 65520) in an "
-                                   "earlier forward; its output is not valid")
+        """Raise if a split-fp16 operand overflowed in any forward since the last check (waits for those forwards; with
+        ``device`` also reads the flag after every stream of it, e.g. forwards of range_guard "off")."""
+        pend, self._range_pending = self._range_pending, []
+        bad = False
+        for snap in pend:
+            bad |= snap.overflowed()
+        if bad:
+            raise RuntimeError(f"RAFT forward: in an earlier forward {_native.RANGE_ERROR}")
         if device is not None:
             _native.range_flag_raise_if_set(device, all_streams=True)
 
@@ -257,10 +268,12 @@ class RAFT(nn.Module):
     ) -> Union[Tensor, Tuple[Tensor, Tensor], List[Tensor]]:
         """Estimate optical flow between pairs of frames (`raft.py:87-147`). Images (B, 3, H, W) in [0, 255]
         with H, W divisible by 8 (use ``InputPadder``). Returns ``(coords1 - coords0, flow_up)`` in test mode,
-        else the list of ``iters`` upsampled predictions. On the GPU in inference, raises RuntimeError when a
-        split-fp16 operand left the fp16 range (``range_guard``)."""
+        else the list of ``iters`` upsampled predictions. On the GPU in inference the split-fp16 range guard
+        (``range_guard``) reports an operand that left the fp16 range with RuntimeError: "sync" raises from this
+        forward; "deferred" (default) does not wait -- this forward's status is ``last_range_snapshot``
+        (``.overflowed()`` waits for it), and a later forward or ``check_range()`` raises for it."""
         guard = self.range_guard in ("sync", "deferred") and image0.is_cuda and not torch.is_grad_enabled()
-        capturing = image0.is_cuda and torch.cuda.is_current_stream_capturing()
+        capturing = image0.is_cuda and capture_active()
         if guard and not capturing:
             self._range_before(image0.device)
         out = self._forward(image0, image1, iters, flow_init, test_mode)
@@ -271,23 +284,24 @@ class RAFT(nn.Module):
     def _range_before(self, dev) -> None:
         """Register the device's range flag; in deferred mode raise for an earlier forward the GPU has finished."""
         _native.range_flag(dev)  # registered before the first kernel that may set it
-        pend = self._range_pending
-        if self.range_guard == "deferred" and pend is not None and pend[1].query():
-            self.check_range()
+        if self.range_guard != "deferred":
+            return
+        bad = False
+        while self._range_pending and self._range_pending[0].done():
+            bad |= self._range_pending.pop(0).overflowed()
+        if bad:
+            raise RuntimeError(f"RAFT forward: in an earlier forward {_native.RANGE_ERROR}")
 
     def _range_after(self, dev) -> None:
-        """After a forward's kernels are enqueued: read the flag now ("sync") or snapshot it ("deferred")."""
+        """After a forward's kernels are enqueued: its snapshot (exchange + copy on the current stream); "sync" waits for
+        it and raises."""
+        snap = _native.RangeSnapshot(torch.device(dev)).take()  # (a new one per forward: callers may hold the last)
+        self.last_range_snapshot = snap
         if self.range_guard == "sync":
-            _native.range_flag_raise_if_set(dev, "RAFT forward")
-        elif self.range_guard == "deferred":
-            pend = self._range_pending
-            if pend is None:
-                pend = (torch.empty(1, dtype=torch.int32, pin_memory=True), torch.cuda.Event(), dev)
-            elif not pend[1].query():
-                return  # the pending snapshot is still in flight; the flag is sticky, the next one will see this forward
-            pend[0].copy_(_native.range_flag(dev), non_blocking=True)
-            pend[1].record(torch.cuda.current_stream(dev))
-            self._range_pending = pend
+            if snap.overflowed():
+                raise RuntimeError(f"RAFT forward: {_native.RANGE_ERROR}")
+        else:
+            self._range_pending.append(snap)
 
     def _forward(self, image0: Tensor, image1: Tensor, iters: int, flow_init: Optional[Tensor], test_mode: bool):
         if (NATIVE_NORMALIZE and image0.is_cuda and image1.is_cuda and image0.dtype == image1.dtype == torch.float32

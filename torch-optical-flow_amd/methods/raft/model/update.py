@@ -194,22 +194,44 @@ def _side_stream(device: torch.device, slot: int = 0) -> "torch.cuda.Stream":
     return _SIDE_STREAMS[key]
 
 
+_CAPTURE_DEPTH = [0]  # > 0 while GraphedRAFT captures a forward (model/graph.py)
+
+
+def capture_active() -> bool:
+    """Whether a HIP graph capture of a forward is in progress. Not ``torch.cuda.is_current_stream_capturing()`` alone:
+    a pair lane's stream joins the capture through an event wait, and on ROCm such a stream does not report itself as
+    capturing, so a check on it alone let the lane wait on an event recorded before the capture -- a dependency the
+    captured graph cannot hold (the two-lane capture crashed in capture_end: profiles/r04/s12_graph8.log)."""
+    return _CAPTURE_DEPTH[0] > 0 or torch.cuda.is_current_stream_capturing()
+
+
+def _module_device(module: nn.Module) -> Optional[torch.device]:
+    for p in module.parameters():
+        return p.device
+    return None
+
+
 def cached_pack(module: nn.Module, key, build):
     """The packed weights cached on ``module`` for ``key`` (built by ``build()`` on a miss). The packing kernels run on
-    the stream current at the miss; an event recorded after them is waited on by every later user's current stream, so a
-    forward issued from another stream (pipelined steps) never reads weights still being written."""
+    the current stream of the module's device at the miss; an event recorded there after them is waited on by every
+    later user's current stream of that device, so a forward issued from another stream (pipelined steps) never reads
+    weights still being written -- also when the module's GPU is not the current device."""
+    dev = _module_device(module)
+    on_gpu = dev is not None and dev.type == "cuda"
     cache = module.__dict__.get("_split_weights")
     if cache is not None and cache[0] == key:
         # (not while a graph is being captured: the capture must not depend on an event recorded outside it; a
         # capture follows warm-up forwards and a device sync, so the weights are complete)
-        if cache[2] is not None and not torch.cuda.is_current_stream_capturing():
-            torch.cuda.current_stream().wait_event(cache[2])
+        if cache[2] is not None and on_gpu and not capture_active():
+            torch.cuda.current_stream(dev).wait_event(cache[2])
         return cache[1]
-    w = build()
-    ev = None
-    if torch.cuda.is_available() and torch.cuda.is_initialized():
-        ev = torch.cuda.Event()
-        ev.record(torch.cuda.current_stream())
+    if on_gpu:
+        with torch.cuda.device(dev):
+            w = build()
+            ev = torch.cuda.Event()
+            ev.record(torch.cuda.current_stream(dev))
+    else:
+        w, ev = build(), None
     module.__dict__["_split_weights"] = (key, w, ev)
     return w
 
@@ -248,7 +270,7 @@ class SplitUpdate:
     """
 
     def __init__(self, block: BasicUpdateBlock, cnet_out: Tensor, hdim: int, side_slot: int = 0,
-                 fuse_c1: bool = True, flow_head_pixels: Optional[int] = None) -> None:
+                 fuse_c1: bool = True, flow_head_pixels: Optional[int] = None, side_owner=None) -> None:
         b, c, h, w = cnet_out.shape
         enc, gru = block.encoder, block.gru
         cdim = c - hdim
@@ -289,7 +311,14 @@ class SplitUpdate:
         self.fuse_c1 = fuse_c1 and "c1L" in self.w
         # side stream for the motion encoder's flow branch (one per device, reused across forwards)
         self.streams = getattr(block, "split_streams", True)
-        self.side_stream = _side_stream(dev, side_slot) if self.streams else None
+        # (keyed by the stream this runner's update() runs on: ``side_owner``, default the current stream)
+        self.side_stream = None
+        if self.streams:
+            if side_owner is None:
+                self.side_stream = _side_stream(dev, side_slot)
+            else:
+                with torch.cuda.stream(side_owner):
+                    self.side_stream = _side_stream(dev, side_slot)
 
     @staticmethod
     def _weights(block: BasicUpdateBlock):

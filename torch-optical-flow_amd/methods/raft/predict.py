@@ -70,8 +70,11 @@ def image_grid(images: List[Tensor], padding: int = 2) -> Tensor:
 
 
 def _write_outputs(event: torch.cuda.Event, flo_path: Path, payload: Tensor, png_path: Optional[Path],
-                   grid: Optional[Tensor]) -> None:
+                   grid: Optional[Tensor], range_snapshot=None) -> None:
     event.synchronize()
+    if range_snapshot is not None and range_snapshot.overflowed():
+        # this pair's forward overflowed a split-fp16 operand: its flow is not valid, so nothing is written for it
+        raise RuntimeError(f"predict: pair {flo_path.stem}: {_native.RANGE_ERROR}")
     h, w = payload.shape[:2]
     with open(flo_path, "wb") as f:
         f.write(np.array([MAGIC_NUMBER], np.float32).tobytes())
@@ -128,6 +131,7 @@ def main(
             padder = InputPadder(img0.shape)
             padded0, padded1 = padder.pad(img0, img1)
             _, flow = model(padded0, padded1, iters=iters, test_mode=True)
+            snap = model.last_range_snapshot  # this pair's own range status, checked by the writer before writing
             assert flow.shape[0] == 1
             flow = padder.unpad(flow)[0]
 
@@ -145,7 +149,7 @@ def main(
                 png = destination / f"{i:06d}.png"
             done = torch.cuda.Event()
             done.record()
-            slot["future"] = writer.submit(_write_outputs, done, destination / f"{i:06d}.flo", payload, png, grid)
+            slot["future"] = writer.submit(_write_outputs, done, destination / f"{i:06d}.flo", payload, png, grid, snap)
             count += 1
         for slot in slots:
             if slot is not None:

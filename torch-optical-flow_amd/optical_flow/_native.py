@@ -75,6 +75,7 @@ SYMBOLS = (
     "oflow_grid_warp_backward_f32",
     "oflow_grid_sample_backward_f32",
     "oflow_set_range_flag",
+    "oflow_range_flag_exchange",
     "oflow_flow_head_col2im_f32",
 )
 
@@ -230,6 +231,8 @@ def load() -> ctypes.CDLL:
     lib.oflow_flow_pack_f32.argtypes = [P, I, I, I, I, I, P, P]
     lib.oflow_set_range_flag.restype = I
     lib.oflow_set_range_flag.argtypes = [P]
+    lib.oflow_range_flag_exchange.restype = I
+    lib.oflow_range_flag_exchange.argtypes = [P, P, P]
     lib.oflow_flow_head_col2im_f32.restype = I
     lib.oflow_flow_head_col2im_f32.argtypes = [P, P, I, I, I, P, P]
     v = lib.oflow_abi_version()
@@ -543,19 +546,53 @@ def range_flag(device: torch.device) -> torch.Tensor:
     return flag
 
 
+class RangeSnapshot:
+    """One forward's split-fp16 range status: the device's range flag exchanged with 0 on the forward's stream right
+    after its kernels (oflow_range_flag_exchange), copied into pinned host memory; ``event`` is recorded after the copy.
+    One per forward."""
+
+    __slots__ = ("dev_word", "host", "event", "device")
+
+    def __init__(self, device: torch.device) -> None:
+        self.device = device
+        self.dev_word = torch.empty(1, dtype=torch.int32, device=device)
+        self.host = torch.empty(1, dtype=torch.int32, pin_memory=True)
+        self.event = torch.cuda.Event()
+
+    def take(self) -> "RangeSnapshot":
+        """Enqueue the exchange + copy on the current stream of the device."""
+        flag = range_flag(self.device)
+        stream = torch.cuda.current_stream(self.device)
+        with torch.cuda.device(self.device):
+            _check(load().oflow_range_flag_exchange(ctypes.c_void_p(flag.data_ptr()),
+                                                    ctypes.c_void_p(self.dev_word.data_ptr()),
+                                                    ctypes.c_void_p(stream.cuda_stream)), "range_flag_exchange")
+            self.host.copy_(self.dev_word, non_blocking=True)
+            self.event.record(stream)
+        return self
+
+    def done(self) -> bool:
+        return self.event.query()
+
+    def overflowed(self) -> bool:
+        """Wait for the snapshot and return whether the forward (or one running concurrently) overflowed."""
+        self.event.synchronize()
+        return bool(int(self.host[0]))
+
+
+RANGE_ERROR = ("a split-fp16 operand exceeded the fp16 range (|x| >= 65520) -- an activation outside the range these "
+               "kernels represent exactly; the output is not valid (OFLOW_CHECK=1 names the convolution)")
+
+
 def range_flag_raise_if_set(device: torch.device, what: str = "RAFT forward", all_streams: bool = False) -> None:
     """Read the device's range flag (one D2H copy of 4 bytes: a sync of the current stream, or of the whole device with
     ``all_streams``: forwards in flight on other streams) and raise if a split-fp16 operand overflowed since the last
     check; the flag is cleared before raising."""
-    flag = range_flag(device)
+    device = torch.device(device)
     if all_streams:
         torch.cuda.synchronize(device)
-    if int(flag.item()):
-        flag.zero_()
-        raise RuntimeError(
-            f"{what}: a split-fp16 operand exceeded the fp16 range (|x| >= 65520) -- an activation outside the range "
-            "these kernels represent exactly; the output is not valid (OFLOW_CHECK=1 names the convolution)"
-        )
+    if RangeSnapshot(device).take().overflowed():  # read and clear in one exchange (nothing set meanwhile is lost)
+        raise RuntimeError(f"{what}: {RANGE_ERROR}")
 
 
 # OFLOW_CHECK=1: before every split-fp16 convolution, a device-side max-abs reduction over its input (the values that
