@@ -423,20 +423,21 @@ def test_range_guard_deferred_mode():
 
 def test_range_snapshot_per_forward():
     """Each GPU inference forward's own range status (RAFT.last_range_snapshot, oflow_range_flag_exchange: the flag read
-    and cleared in one device-side exchange after the forward's kernels): an overflowing forward followed by a valid one
-    -- neither waited on -- report True and False respectively, and the deferred check then raises once."""
+    and cleared in one device-side exchange after the forward's kernels): an overflowing forward's snapshot reports
+    True; the next forward (deferred mode) first raises for it, and a valid forward after that reports False with
+    nothing left set on the device."""
     img0, img1 = synthetic.synthetic_pair(1, 128, 160, seed=6)
     p0, p1 = img0.to(DEV), img1.to(DEV)
     m = _model(RAFT)
     with torch.inference_mode():
         m(p0 * 1e6, p1 * 1e6, iters=2, test_mode=True)
         bad = m.last_range_snapshot
+        assert bad.overflowed()
+        with pytest.raises(RuntimeError, match="fp16 range"):
+            m(p0, p1, iters=2, test_mode=True)  # reports the earlier forward before running
         m(p0, p1, iters=2, test_mode=True)
         good = m.last_range_snapshot
-        assert bad is not good
-        assert bad.overflowed() and not good.overflowed()
-        with pytest.raises(RuntimeError, match="fp16 range"):
-            m.check_range()
+        assert good is not bad and not good.overflowed()
         m.check_range(DEV)  # nothing left set
 
 

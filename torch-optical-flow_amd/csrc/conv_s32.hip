@@ -772,7 +772,16 @@ __global__ __launch_bounds__(64 * WM * WN, WM * WN == 8 ? 1 : 2) void conv_s32_k
   __syncthreads();
   if (has_add) {
     // pre-activation value = acc * scale + bias + addend, in place (each thread rewrites only its own items, which it
-    // alone reads below: no barrier)
+    // alone reads below: no barrier). r05: the item's 8 tile values as two 16-B LDS accesses each way (the main
+    // epilogue loop's conflict-free pattern) and the channel octet's (scale, bias) read once -- the scalar form (8 + 8
+    // dword accesses per item, 16 lanes of a pixel 8 floats apart: 4-way bank conflicts) was the GRU kernels' 0.14 /
+    // 0.20 LDS-conflict rate (profiles/r04/s28_pmc_mfma.json)
+    constexpr bool FIXED_OCT_ADD = NTH % C8 == 0;
+    float2 sba[8];
+    if constexpr (FIXED_OCT_ADD) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) sba[j] = sSB[(tid % C8) * 8 + j];
+    }
 #pragma unroll
     for (int k = 0; k < (EPI == 0 ? 0 : KIT); ++k) {
       const int item = tid + k * NTH;
@@ -780,12 +789,16 @@ __global__ __launch_bounds__(64 * WM * WN, WM * WN == 8 ? 1 : 2) void conv_s32_k
       const int y = ty0 + pl / kTX, x = tx0 + (pl % kTX);
       if (item >= BM * C8 || n >= a.N || y >= a.H || x >= a.W) continue;
       const float* av = reinterpret_cast<const float*>(&ad[k][0]);
-      float* tp = &sT[pl * TS + nl];
+      float4* tp4 = reinterpret_cast<float4*>(&sT[pl * TS + nl]);
+      const float4 t0 = tp4[0], t1 = tp4[1];
+      float t[8] = {t0.x, t0.y, t0.z, t0.w, t1.x, t1.y, t1.z, t1.w};
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
-        const float2 sb = sSB[nl + j];
-        tp[j] = (tp[j] * sb.x + sb.y) + av[j];
+        const float2 sb = FIXED_OCT_ADD ? sba[j] : sSB[nl + j];
+        t[j] = (t[j] * sb.x + sb.y) + av[j];
       }
+      tp4[0] = make_float4(t[0], t[1], t[2], t[3]);
+      tp4[1] = make_float4(t[4], t[5], t[6], t[7]);
     }
   }
 

@@ -964,6 +964,314 @@ __global__ __launch_bounds__(256, 2) void corr_convc1_pipe_kernel(C1Args a) {
   stamp();
 }
 
+// r05 VALU-lean kernel (4 waves, 64 queries, two workgroups per CU; the r04 kernel's level pipeline). PMC of the r04
+// kernel (profiles/r05/s4_pmc_mfma.json): 4,751 VALU instructions per wave, ~1,190 per level, against 72 MFMAs per
+// level; a wave64 VALU instruction occupies its SIMD for ~4 cycles, so with two waves per SIMD the VALU alone is ~9.5 k
+// of a level's ~12 k cycles (stamps, s4_stamps.log) -- the kernel was VALU-issue bound, not gather or MFMA bound. ISA
+// count: ~32 VALU to address each 16-B window chunk load and ~36 to write it to the patch (item decode, window origin,
+// tile arithmetic, validity masks, the zero selects), i.e. ~680 of the ~1,190 per level. Here:
+//   * the decoding wave writes, per (query, level), the byte offset of each of the window's PK rows in the tiled level
+//     (query base folded in) and of each of its NCH chunk columns, with a sentinel (2^30) for rows / chunks outside the
+//     level or the window: a chunk's offset is one add of two LDS words, and an outside chunk's offset lies past the
+//     buffer's size, so the buffer load returns zeros without touching memory (the zero padding of Q4 for free);
+//   * every thread's chunk items (query, row, chunk) are decoded once into one packed register per item;
+//   * the patch write is then the item's constant offset + the query's window base, and four stores, no selects (only
+//     levels whose width is not a multiple of 4 -- a chunk partly past the level's right edge -- take a masked path);
+//   * the MFMA runs with the operands swapped and the epilogue stores from the accumulators (no LDS tile).
+// Same chunk data, taps, products and order: bit-identical to the r04 kernel.
+template <int R>
+__global__ __launch_bounds__(256, 2) void corr_convc1_lean_kernel(C1Args a) {
+  constexpr int NT = 256;
+  constexpr int PK = 2 * R + 2, K = 2 * R + 1, KK = K * K;
+  constexpr int NCH = (PK + 6) / 4;
+  constexpr int RW = ((4 * NCH > PK + 3) ? 4 * NCH : PK + 3) | 1;
+  constexpr int QS = ((PK * RW + 3) | 1);
+  constexpr int G = (KK + 31) / 32;
+  constexpr int NSLOT = (KK + 7) / 8;
+  constexpr int A_BYTES = G * kQM * 128;
+  constexpr int P_BYTES = kQM * QS * 4;
+  constexpr int CITEMS = kQM * PK * NCH;
+  constexpr int NI = (CITEMS + NT - 1) / NT;
+  constexpr int NS = 2;                      // decode slots (level & 1): level l+1 decoded while level l's patch is written
+  constexpr int SENT = 1 << 30;              // offset sentinel: past any workgroup's buffer size
+  static_assert(kQM * PK <= 1024 && kQM * NCH <= 256 && 9 * RW + 4 * NCH <= 255, "packed item fields");
+  __shared__ __attribute__((aligned(16))) uint8_t smem[A_BYTES + P_BYTES];
+  __shared__ int sRow[NS][kQM * PK];   // byte offset of window row u of query q in the level (+ q * LF * 4), or SENT
+  __shared__ int sCol[NS][kQM * NCH];  // byte offset of window chunk column k, or SENT
+  __shared__ int sPB[NS][kQM];         // the query's patch base: q * QS + 3 - dx
+  __shared__ int sXA[NS][kQM];         // the window's first chunk column x0 & ~3 (masked path only)
+  __shared__ float4 sW[NS][kQM];       // bilinear weights (nw, ne, sw, se)
+  __shared__ float2 sC[kQM];
+  uint8_t* sA = smem;
+  float* sP = reinterpret_cast<float*>(smem + A_BYTES);
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int r = lane & 31, hh = lane >> 5;
+  const int q0 = blockIdx.x * kQM;
+  const int nq = min(kQM, a.total - q0);
+  const int L = a.nlev;
+  int nst = 0;
+  auto stamp = [&]() {
+    if (a.stamps != nullptr) {
+      if (tid == 0) a.stamps[(size_t)blockIdx.x * 16 + nst] = __builtin_amdgcn_s_memtime();
+      ++nst;
+    }
+  };
+  stamp();
+  auto level = [&](int l, int& Hl, int& Wl, int& WB, int& LF, const float*& base) {
+    Hl = a.Hl[0]; Wl = a.Wl[0]; WB = a.WB[0]; LF = a.LF[0]; base = a.lv[0];
+#pragma unroll
+    for (int j = 1; j < OFLOW_MAX_LEVELS; ++j)
+      if (j == l) { Hl = a.Hl[j]; Wl = a.Wl[j]; WB = a.WB[j]; LF = a.LF[j]; base = a.lv[j]; }
+  };
+  // window of query `lane` at level l -> the offset tables of slot l & 1 (one wave; lane = query)
+  auto decode = [&](int l, float cx, float cy) __attribute__((always_inline)) {
+    int Hl, Wl, WB, LF;
+    const float* base;
+    level(l, Hl, Wl, WB, LF, base);
+    int xs, ys;
+    float4 w4;
+    window_origin(cx, cy, __int_as_float((127 - l) << 23), R, xs, ys, w4);  // 1/2^l exactly (corr.py:68)
+    const int dx = xs & 3, xa = xs - dx;
+    const int sl = l & (NS - 1), q = lane;
+    const int qb = q * LF * 4;
+#pragma unroll
+    for (int u = 0; u < PK; ++u) {
+      const int y = ys + u;
+      sRow[sl][q * PK + u] = static_cast<unsigned>(y) < static_cast<unsigned>(Hl)
+                                 ? qb + (y >> 2) * (WB * 128) + ((y & 3) << 5) : SENT;
+    }
+#pragma unroll
+    for (int k = 0; k < NCH; ++k) {
+      const int xc = xa + 4 * k;
+      sCol[sl][q * NCH + k] = (static_cast<unsigned>(xc) < static_cast<unsigned>(Wl) && 4 * k < dx + PK)
+                                  ? ((xc >> 3) << 7) + ((xc & 7) << 2) : SENT;
+    }
+    sPB[sl][q] = q * QS + 3 - dx;
+    sXA[sl][q] = xa;
+    sW[sl][q] = w4;
+  };
+  if (wave == 0) {
+    float cx = 1e30f, cy = 1e30f;  // past the last query: all-zero window
+    if (lane < nq) {
+      const int qq = q0 + lane;
+      const int b = qq / a.N, pix = qq - b * a.N;
+      cx = a.coords[(size_t)(2 * b) * a.N + pix];
+      cy = a.coords[(size_t)(2 * b + 1) * a.N + pix];
+    }
+    sC[lane] = make_float2(cx, cy);
+    decode(0, cx, cy);
+  }
+  for (int e = tid; e < A_BYTES / 16; e += NT) reinterpret_cast<u32x4*>(sA)[e] = u32x4{0u, 0u, 0u, 0u};
+  // chunk item s of this thread -> bits 0-9 q*PK + u, 10-17 q*NCH + k, 18-25 u*RW + 4k (recomputed per use from an
+  // opaque copy of tid: a few full-rate ops, no registers held across the level)
+  static_assert(magic16_ok(PK * NCH, CITEMS) && magic16_ok(NCH, PK * NCH), "chunk item decode");
+  auto item_word = [&](int s) __attribute__((always_inline)) {
+    int t_ = tid;
+    asm volatile("" : "+v"(t_));
+    const unsigned item = static_cast<unsigned>(min(t_ + NT * s, CITEMS - 1));
+    const unsigned q = __umul24(item, magic16(PK * NCH)) >> 16;
+    const unsigned rm = item - q * (PK * NCH);
+    const unsigned u = (NCH == 4) ? (rm >> 2) : (__umul24(rm, magic16(NCH)) >> 16);
+    const unsigned k = rm - u * NCH;
+    return (q * PK + u) | ((q * NCH + k) << 10) | ((u * RW + 4 * k) << 18);
+  };
+  __syncthreads();
+  u32x4 rv[NI];
+  auto gather = [&](int l) __attribute__((always_inline)) {
+    int Hl, Wl, WB, LF;
+    const float* base;
+    level(l, Hl, Wl, WB, LF, base);
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<float*>(base + (size_t)q0 * LF), (short)0, nq * LF * 4, 0x00020000);
+    const int sl = l & (NS - 1);
+    int ro[NI], co[NI];  // all table reads first (one LDS round trip), then the loads
+#pragma unroll
+    for (int s = 0; s < NI; ++s) {
+      const unsigned w = item_word(s);
+      ro[s] = sRow[sl][w & 1023u];
+      co[s] = sCol[sl][(w >> 10) & 255u];
+    }
+#pragma unroll
+    for (int s = 0; s < NI; ++s) rv[s] = __builtin_amdgcn_raw_buffer_load_b128(rs, ro[s] + co[s], 0, 0);
+  };
+  // chunks -> patch row u of query q at sP[q*QS + u*RW], the window's cells at +3 .. (a chunk's cells at
+  // +3 + 4k - dx + e; outside chunks arrived as zeros). A level whose width is not a multiple of 4 masks the cells of a
+  // chunk past its right edge (tile padding).
+  auto patch_write = [&](int l) __attribute__((always_inline)) {
+    int Hl, Wl, WB, LF;
+    const float* base;
+    level(l, Hl, Wl, WB, LF, base);
+    const int sl = l & (NS - 1);
+    const bool ragged = (Wl & 3) != 0;
+    int pb[NI];  // the queries' patch bases first (one LDS round trip)
+#pragma unroll
+    for (int s = 0; s < NI; ++s) pb[s] = sPB[sl][(item_word(s) & 1023u) / PK];
+#pragma unroll
+    for (int s = 0; s < NI; ++s) {
+      if (CITEMS % NT == 0 || tid + NT * s < CITEMS) {
+        const unsigned w = item_word(s);
+        const unsigned q = (w & 1023u) / PK;
+        float4 f4 = __builtin_bit_cast(float4, rv[s]);
+        if (ragged) {
+          const int k = static_cast<int>((w >> 10) & 255u) - static_cast<int>(q) * NCH;
+          const int nv = Wl - (sXA[sl][q] + 4 * k);
+          f4.y = nv > 1 ? f4.y : 0.f;
+          f4.z = nv > 2 ? f4.z : 0.f;
+          f4.w = nv > 3 ? f4.w : 0.f;
+        }
+        float* dst = sP + pb[s] + (w >> 18);
+        dst[0] = f4.x;
+        dst[1] = f4.y;
+        dst[2] = f4.z;
+        dst[3] = f4.w;
+      }
+    }
+  };
+  const __amdgpu_buffer_rsrc_t rsW =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(a.wf), (short)0, L * G * kN * 128, 0x00020000);
+  const int wbase = wave * 8192 + lane * 16;
+  u32x4 bq[2][8];
+  auto load_b = [&](int t, u32x4 (&dst)[8]) __attribute__((always_inline)) {
+    const int so = t * (kN * 128);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) dst[e] = __builtin_amdgcn_raw_buffer_load_b128(rsW, wbase, so + e * 1024, 0);
+  };
+  f32x16 acc[2][2];  // [nt][mt]: C[channel][pixel]
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
+
+  const int nlg = L * G;
+  load_b(0, bq[0]);
+  if (nlg > 1) load_b(1, bq[1]);
+  gather(0);
+  stamp();
+  auto body = [&](int l, auto Pc) __attribute__((always_inline)) {
+    constexpr int P = decltype(Pc)::value;
+    // ---- 1. chunks -> LDS patches; the next level's windows decoded (slot (l+1) & 1: level l-1's, free) ----
+    patch_write(l);
+    if (wave == 3 && l + 1 < L) decode(l + 1, sC[lane].x, sC[lane].y);
+    __syncthreads();  // patches and level l+1's tables complete; every wave is past level l-1's MFMAs (A free)
+    stamp();
+    // ---- 2. next level's gathers (rv is free) ----
+    if (l + 1 < L) gather(l + 1);
+    // ---- 3. bilinear taps -> split-fp16 tap operand; the slot set is the wave index ----
+    {
+      const int q = lane, set = __builtin_amdgcn_readfirstlane(wave);
+      const float4 w4 = sW[l & (NS - 1)][q];
+      const float* p = sP + q * QS + 3;
+#pragma unroll
+      for (int S = 0; S < NSLOT; ++S) {
+        if ((S & 3) != set) continue;
+        float v[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const int k = 8 * S + e;  // reference channel order within the level: k = i*K + j, i moves x, j moves y
+          v[e] = 0.f;
+          if (k < KK) {
+            const int i = k / K, j = k - (k / K) * K;
+            v[e] = bilinear4(p[j * RW + i], p[j * RW + i + 1], p[(j + 1) * RW + i], p[(j + 1) * RW + i + 1], w4);
+          }
+        }
+        range_guard8(v);
+        half8 hi, lo;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          _Float16 h_, l_;
+          split_f16(v[e], h_, l_);
+          hi[e] = h_;
+          lo[e] = l_;
+        }
+        uint8_t* row = sA + (S >> 2) * (kQM * 128) + q * 128;
+        *reinterpret_cast<half8*>(row + (((S & 3) ^ swz(q)) << 4)) = hi;
+        *reinterpret_cast<half8*>(row + (((4 + (S & 3)) ^ swz(q)) << 4)) = lo;
+      }
+    }
+    __syncthreads();  // tap operand complete; the patches consumed
+    stamp();
+    // ---- 4. the level's MFMAs: C[channel][pixel] += W[channel][k] * T[k][pixel] ----
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+      u32x4 (&wc)[8] = bq[(P + g) & 1];
+#pragma unroll
+      for (int sub = 0; sub < 2; ++sub) {
+        half8 th[2], tl[2];
+        const int chi = 2 * sub + hh, clo = 4 + 2 * sub + hh;
+#pragma unroll
+        for (int mt = 0; mt < 2; ++mt) {
+          const int pr = mt * 32 + r;
+          const uint8_t* row = sA + g * (kQM * 128) + pr * 128;
+          th[mt] = *reinterpret_cast<const half8*>(row + ((chi ^ swz(pr)) << 4));
+          tl[mt] = *reinterpret_cast<const half8*>(row + ((clo ^ swz(pr)) << 4));
+        }
+#pragma unroll
+        for (int nt = 0; nt < 2; ++nt) {
+          const half8 wh = __builtin_bit_cast(half8, wc[(nt * 2 + sub) * 2 + 0]);
+          const half8 wl = __builtin_bit_cast(half8, wc[(nt * 2 + sub) * 2 + 1]);
+#pragma unroll
+          for (int mt = 0; mt < 2; ++mt) {
+            acc[nt][mt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(wl, th[mt], acc[nt][mt], 0, 0, 0);
+            acc[nt][mt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(wh, tl[mt], acc[nt][mt], 0, 0, 0);
+            acc[nt][mt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(wh, th[mt], acc[nt][mt], 0, 0, 0);
+          }
+        }
+      }
+      const int t2 = l * G + g + 2;
+      if (t2 < nlg) load_b(t2, wc);
+    }
+    stamp();
+  };
+  for (int l = 0; l < L; l += 2) {
+    body(l, std::integral_constant<int, 0>{});
+    if (l + 1 < L) body(l + 1, std::integral_constant<int, G & 1>{});
+  }
+
+  // ---- epilogue from the accumulators: lane (pixel r of tile mt, half hh) holds channels 8j + 4hh + e of tile nt ----
+  typedef _Float16 half4 __attribute__((ext_vector_type(4)));
+  float mx = 0.f;
+#pragma unroll
+  for (int nt = 0; nt < 2; ++nt) {
+    const int cb = wave * 64 + nt * 32;  // S32 group 2 * wave + nt
+    float4 sc[4], bi[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      sc[j] = *reinterpret_cast<const float4*>(a.wsc + cb + 8 * j + 4 * hh);
+      bi[j] = a.bias ? *reinterpret_cast<const float4*>(a.bias + cb + 8 * j + 4 * hh) : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+#pragma unroll
+    for (int mt = 0; mt < 2; ++mt) {
+      const int pl = mt * 32 + r;
+      if (pl >= nq) continue;
+      uint8_t* line = a.y + (long long)(q0 + pl) * a.yps + (cb >> 5) * 128;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float s4[4] = {sc[j].x, sc[j].y, sc[j].z, sc[j].w};
+        const float b4[4] = {bi[j].x, bi[j].y, bi[j].z, bi[j].w};
+        half4 hi, lo;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          float x = acc[nt][mt][j * 4 + e] * s4[e] + b4[e];
+          x = x < 0.f ? 0.f : x;  // relu (update.py:120); NaN propagates like ATen
+          mx = fmaxf(mx, x);
+          _Float16 h_, l_;
+          split_f16(x, h_, l_);
+          hi[e] = h_;
+          lo[e] = l_;
+        }
+        *reinterpret_cast<half4*>(line + (8 * j + 4 * hh) * 2) = hi;
+        *reinterpret_cast<half4*>(line + 64 + (8 * j + 4 * hh) * 2) = lo;
+      }
+    }
+  }
+  range_guard(mx);
+  if (a.stamps != nullptr) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  stamp();
+}
+
 unsigned long long* g_convc1_stamps = nullptr;  // diagnostics (experiment hook): per-workgroup clock stamps
 int g_convc1_variant = 1;  // 1: the r04 4-wave kernel (default), 2: the 8-wave kernel, 3: the pipelined kernel (experiment hook)
 
@@ -1011,6 +1319,11 @@ extern "C" int oflow_corr_lookup_convc1_s32(const float* const* d_levels, const 
       hipLaunchKernelGGL((corr_convc1_kernel<4>), grid, dim3(kNT), 0, s, a);
     else
       hipLaunchKernelGGL((corr_convc1_kernel<3>), grid, dim3(kNT), 0, s, a);
+  } else if (g_convc1_variant == 4) {
+    if (radius == 4)
+      hipLaunchKernelGGL((corr_convc1_lean_kernel<4>), grid, dim3(256), 0, s, a);
+    else
+      hipLaunchKernelGGL((corr_convc1_lean_kernel<3>), grid, dim3(256), 0, s, a);
   } else if (g_convc1_variant == 3) {
     if (radius == 4)
       hipLaunchKernelGGL((corr_convc1_pipe_kernel<4>), grid, dim3(256), 0, s, a);
