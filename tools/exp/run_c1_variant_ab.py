@@ -1,5 +1,5 @@
-"""In-process A/B of the fused lookup + convc1 kernel variants of this library (oflow_exp_set_convc1_variant: 1 = the
-4-wave kernel, 2 = the 8-wave kernel): same inputs (Sintel 55x128 grid, N(0, 4^2) px flow, three pyramids in rotation,
+"""In-process A/B of the fused lookup + convc1 kernel (variant 1: the product, liboflow_hip.so) and its experiment
+variants (2-5: tools/exp/corr_convc1_variants.hip -> build/exp/libc1var.so, tools/exp/build_c1var.sh): same inputs (Sintel 55x128 grid, N(0, 4^2) px flow, three pyramids in rotation,
 cold), 8 pairs (one launch) and 4 pairs (one pair lane); interleaved rounds. Reports whether the outputs are bit-identical
 and the largest difference of the S32 values (hi + lo) otherwise.
     python tools/exp/run_c1_variant_ab.py"""
@@ -20,19 +20,50 @@ from model import synthetic  # noqa: E402
 from model.utils import coords_grid  # noqa: E402
 
 DEV = torch.device("cuda", 0)
-VARIANTS = [int(v) for v in os.environ.get("VARIANTS", "1,2,3").split(",")]
+VARIANTS = [int(v) for v in os.environ.get("VARIANTS", "1,2,3,4,5").split(",")]
 
 
-def timeit(fn, reps=20):
+def timeit(fn, reps=20, burst=5):
+    """median GPU time per launch (us) of `burst` back-to-back launches queued behind a spin kernel, so the host's
+    launch overhead (the product wrapper's Python checks vs a bare ctypes call) is not in the events' interval"""
     ts = []
     for _ in range(reps):
         a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        torch.cuda._sleep(2_000_000)
         a.record()
-        fn()
+        for _ in range(burst):
+            fn()
         b.record()
         torch.cuda.synchronize()
-        ts.append(a.elapsed_time(b) * 1e3)
+        ts.append(a.elapsed_time(b) * 1e3 / burst)
     return statistics.median(ts)
+
+
+def variant_caller(N, cw, coords, b, h, w):
+    """call(v, pyr, y, stamps=None): variant 1 = the product kernel (N.corr_lookup_convc1; stamps through the product's
+    hook), variants 2-5 = build/exp/libc1var.so (tools/exp/build_c1var.sh), same arguments."""
+    exp = ctypes.CDLL(os.path.join(REPO, "build", "exp", "libc1var.so"))
+    exp.oflow_exp_convc1_variant.restype = ctypes.c_int
+    P, I = ctypes.c_void_p, ctypes.c_int
+    exp.oflow_exp_convc1_variant.argtypes = [I, ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(I), ctypes.POINTER(I), I, P,
+                                             I, I, I, I, P, P, P, P, ctypes.c_longlong, P, P]
+    lib = N.load()
+    lib.oflow_exp_set_convc1_stamps.argtypes = [ctypes.c_void_p]
+
+    def call(v, pyr, y, stamps=None):
+        if v == 1:
+            lib.oflow_exp_set_convc1_stamps(stamps)
+            N.corr_lookup_convc1(pyr, coords, 4, cw, N.S32Slice(y))
+            lib.oflow_exp_set_convc1_stamps(None)
+            return
+        ptrs = (ctypes.c_void_p * N.MAX_LEVELS)(*[t.data_ptr() for t in pyr.levels])
+        hs = (ctypes.c_int * N.MAX_LEVELS)(*[d[0] for d in pyr.dims])
+        ws = (ctypes.c_int * N.MAX_LEVELS)(*[d[1] for d in pyr.dims])
+        st = exp.oflow_exp_convc1_variant(v, ptrs, hs, ws, 4, coords.data_ptr(), b, h, w, 4, cw.pack.data_ptr(),
+                                          cw.wscale.data_ptr(), cw.bias.data_ptr(), y.data_ptr(), 8 * 128, stamps,
+                                          ctypes.c_void_p(torch.cuda.current_stream().cuda_stream))
+        assert st == 0, st
+    return call
 
 
 def s32_values(y):
@@ -42,8 +73,6 @@ def s32_values(y):
 
 
 def main():
-    lib = N.load()
-    lib.oflow_exp_set_convc1_variant.argtypes = [ctypes.c_int]
     h, w = 55, 128
     conv = torch.nn.Conv2d(324, 256, 1).to(DEV)
     with torch.no_grad():
@@ -58,10 +87,10 @@ def main():
         coords = (coords_grid(b, h, w) + torch.from_numpy(synthetic.hash_normal(9, (b, 2, h, w), 4.0))).to(DEV).contiguous()
         ys = {v: N.s32_empty(b, h, w, 8, DEV) for v in VARIANTS}
         it = [0]
+        vcall = variant_caller(N, cw, coords, b, h, w)
 
         def call(v, pyr):
-            lib.oflow_exp_set_convc1_variant(v)
-            N.corr_lookup_convc1(pyr, coords, 4, cw, N.S32Slice(ys[v]))
+            vcall(v, pyr, ys[v])
 
         def arm(v):
             def f():
@@ -89,7 +118,6 @@ def main():
         out[f"pairs{b}"] = {f"v{k}": {"min": round(min(x), 2), "median": round(statistics.median(x), 2)} for k, x in res.items()}
         out[f"pairs{b}"]["bit_identical"] = same
         out[f"pairs{b}"]["max_rel_diff_of_max"] = maxd
-    lib.oflow_exp_set_convc1_variant(2)
     print(json.dumps({"us": out}))
 
 
