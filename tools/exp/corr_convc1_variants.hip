@@ -3,7 +3,7 @@
 // ("corr_convc1 ... r05") and profiles/r05/s2-s7. Built as a separate library (tools/exp/build_c1var.sh ->
 // build/exp/libc1var.so) with one C entry point taking the product ABI's arguments plus the variant number, so that the
 // A/B scripts (tools/exp/run_c1_variant_ab.py, run_c1_stamps_variants.py) time them in one process beside the product.
-// Variants: 2 = 8 waves; 3 = phase-pipelined; 4 = VALU-lean (offset tables, register epilogue); 5 = hybrid. Every one is
+// Variants: 2 = 8 waves; 3 = phase-pipelined; 4 = VALU-lean (offset tables, register epilogue); 5 = hybrid; 6 = rowmap; 7 = quad; 8 = 128 queries per workgroup. Every one is
 // bit-identical to the product kernel (checked by the A/B script on three pyramids).
 #include <type_traits>
 #include <utility>
@@ -1285,7 +1285,868 @@ __global__ __launch_bounds__(256, 2) void corr_convc1_hyb_kernel(C1Args a) {
 }
 
 
+// r05 variant 6 ("rowmap"): the r04 kernel with the two VALU-heavy parts rebuilt (PMC: 4,751 VALU per wave, ~680 of a
+// level's ~1,190 for chunk addressing and patch writes, ~8 per tap for the hi/lo split):
+//   * chunk gathers mapped as thread = (query q = tid / 4, chunk column k = tid % 4) x every window row u: the column's
+//     byte offset (query base folded in, or a sentinel past the buffer when the column is outside the level or not
+//     needed) is formed once per level, each row adds its tile-row / row-in-tile part and is replaced by the sentinel
+//     when outside the level (the buffer load then returns zeros without a memory access: Q4's zero padding); the patch
+//     write of row u is four ds_write_b32 at immediate offsets from one per-level base (q*QS + 3 - dx + 4k). A level
+//     whose width is not a multiple of 4 masks the cells of the one chunk column that crosses its right edge.
+//   * split: hi pairs by v_cvt_pk_f16_f32 (RNE), lo = fp16(v - hi) by v_fma_mixlo/mixhi_f16 (v - hi is exact in fp32,
+//     so one rounding of the exact difference = the cvt(sub) pair's result), three VALU per two taps instead of ~8.
+// Taps, products, order and epilogue as the r04 kernel: bit-identical.
+// split_lo_pair: oflow_internal.h
+
+template <int R>
+__global__ __launch_bounds__(kNT, 2) void corr_convc1_rowmap_kernel(C1Args a) {
+  constexpr int PK = 2 * R + 2, K = 2 * R + 1, KK = K * K;
+  constexpr int NCH = (PK + 6) / 4;
+  constexpr int RW = ((4 * NCH > PK + 3) ? 4 * NCH : PK + 3) | 1;
+  constexpr int QS = ((PK * RW + 3) | 1);
+  constexpr int G = (KK + 31) / 32;
+  constexpr int NSLOT = (KK + 7) / 8;
+  constexpr int A_BYTES = G * kQM * 128;
+  constexpr int P_BYTES = kQM * QS * 4;
+  constexpr int TS = kN + 4;
+  constexpr int EPI_BYTES = kQM * TS * 4;
+  constexpr int MAIN = A_BYTES + P_BYTES;
+  constexpr int LDS_BYTES = MAIN > EPI_BYTES ? MAIN : EPI_BYTES;
+  constexpr int NS = 4;
+  constexpr unsigned SENT = 0x80000000u;  // past any workgroup's buffer (< 2^31 bytes): the load returns zeros
+  static_assert(NCH <= 4 && kNT == 4 * kQM, "thread = (query, chunk column)");
+  static_assert(3 + 4 * NCH - 1 + (PK - 1) * RW < QS, "a row's chunks stay inside the query's patch");
+  __shared__ __attribute__((aligned(16))) uint8_t smem[LDS_BYTES];
+  __shared__ float2 sSB[kN];
+  __shared__ float2 sC[kQM];
+  __shared__ int4 sO[NS][kQM];    // window origin x0, y0, (unused), dx
+  __shared__ float4 sW[NS][kQM];  // bilinear weights (nw, ne, sw, se)
+  uint8_t* sA = smem;
+  float* sP = reinterpret_cast<float*>(smem + A_BYTES);
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wn = wave;
+  const int r = lane & 31, hh = lane >> 5;
+  const int q0 = blockIdx.x * kQM;
+  const int nq = min(kQM, a.total - q0);
+  const int gq = tid >> 2, gk = tid & 3;  // the gather role: query, chunk column
+  int nst = 0;
+  auto stamp = [&]() {
+    if (a.stamps != nullptr) {
+      if (tid == 0) a.stamps[(size_t)blockIdx.x * 16 + nst] = __builtin_amdgcn_s_memtime();
+      ++nst;
+    }
+  };
+  stamp();
+  auto level = [&](int l, int& Hl, int& Wl, int& WB, int& LF, const float*& base) {
+    Hl = a.Hl[0]; Wl = a.Wl[0]; WB = a.WB[0]; LF = a.LF[0]; base = a.lv[0];
+#pragma unroll
+    for (int j = 1; j < OFLOW_MAX_LEVELS; ++j)
+      if (j == l) { Hl = a.Hl[j]; Wl = a.Wl[j]; WB = a.WB[j]; LF = a.LF[j]; base = a.lv[j]; }
+  };
+  const int qd = tid & (kQM - 1);
+  const bool dwave = tid >= (kNT - kQM);
+  auto decode = [&](int l, float cx, float cy) {
+    int xs, ys;
+    float4 w4;
+    window_origin(cx, cy, __int_as_float((127 - l) << 23), R, xs, ys, w4);  // 1/2^l exactly (corr.py:68)
+    sO[l & (NS - 1)][qd] = make_int4(xs, ys, 0, xs & 3);
+    sW[l & (NS - 1)][qd] = w4;
+  };
+
+  for (int c = tid; c < kN; c += kNT) sSB[c] = make_float2(a.wsc[c], a.bias ? a.bias[c] : 0.f);
+  if (wave < 2) {
+    float2 c = make_float2(1e30f, 1e30f);  // past the last query: all-zero window
+    if (qd < nq) {
+      const int q = q0 + qd;
+      const int b = q / a.N, pix = q - b * a.N;
+      c = make_float2(a.coords[(size_t)(2 * b) * a.N + pix], a.coords[(size_t)(2 * b + 1) * a.N + pix]);
+    }
+    if (wave == 0) sC[qd] = c;
+    if (wave < a.nlev) decode(wave, c.x, c.y);
+  }
+  for (int e = tid; e < A_BYTES / 16; e += kNT) reinterpret_cast<u32x4*>(sA)[e] = u32x4{0u, 0u, 0u, 0u};
+  __syncthreads();
+
+  u32x4 rv[PK];
+  auto gather = [&](int l) {
+    int Hl, Wl, WB, LF;
+    const float* base;
+    level(l, Hl, Wl, WB, LF, base);
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<float*>(base + (size_t)q0 * LF), (short)0, nq * LF * 4, 0x00020000);
+    if (NCH == 4 || gk < NCH) {
+      const int4 o = sO[l & (NS - 1)][gq];
+      const int xc = o.x - o.w + 4 * gk;
+      const bool cv = static_cast<unsigned>(xc) < static_cast<unsigned>(Wl) && 4 * gk < o.w + PK;
+      const unsigned cb = cv ? static_cast<unsigned>(__umul24(gq, LF) * 4 + ((xc >> 3) << 7) + ((xc & 7) << 2)) : SENT;
+      const int WB128 = WB * 128;
+#pragma unroll
+      for (int u = 0; u < PK; ++u) {
+        const int y = o.y + u;
+        unsigned off = cb + static_cast<unsigned>(__mul24(y >> 2, WB128) + ((y & 3) << 5));
+        off = static_cast<unsigned>(y) < static_cast<unsigned>(Hl) ? off : SENT;
+        rv[u] = __builtin_amdgcn_raw_buffer_load_b128(rs, static_cast<int>(off), 0, 0);
+      }
+    }
+  };
+  const __amdgpu_buffer_rsrc_t rsW =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(a.wf), (short)0, a.nlev * G * kN * 128, 0x00020000);
+  const int wbase = wn * 8192 + lane * 16;
+  u32x4 bq[2][8];
+  auto load_b = [&](int t, u32x4 (&dst)[8]) {
+    const int so = t * (kN * 128);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) dst[e] = __builtin_amdgcn_raw_buffer_load_b128(rsW, wbase, so + e * 1024, 0);
+  };
+  f32x16 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
+
+  const int nlg = a.nlev * G;
+  load_b(0, bq[0]);
+  if (nlg > 1) load_b(1, bq[1]);
+  gather(0);
+  stamp();
+  auto body = [&](int l, auto Pc) {
+    constexpr int P = decltype(Pc)::value;
+    // ---- 1. chunks -> LDS patches ----
+    if (NCH == 4 || gk < NCH) {
+      int Hl, Wl, WB, LF;
+      const float* base;
+      level(l, Hl, Wl, WB, LF, base);
+      const int4 o = sO[l & (NS - 1)][gq];
+      int dofs = (A_BYTES / 4) + gq * QS + 3 - o.w + 4 * gk;
+      asm volatile("" : "+v"(dofs));  // one base register, immediate offsets
+      float* dst = reinterpret_cast<float*>(smem) + dofs;
+      if (Wl & 3) {  // the chunk column crossing the right edge: cells past it are tile padding
+        const int nv = Wl - (o.x - o.w + 4 * gk);
+#pragma unroll
+        for (int u = 0; u < PK; ++u) {
+          const float* fv = reinterpret_cast<const float*>(&rv[u]);
+          dst[u * RW + 0] = fv[0];
+          dst[u * RW + 1] = nv > 1 ? fv[1] : 0.f;
+          dst[u * RW + 2] = nv > 2 ? fv[2] : 0.f;
+          dst[u * RW + 3] = nv > 3 ? fv[3] : 0.f;
+        }
+      } else {
+#pragma unroll
+        for (int u = 0; u < PK; ++u) {
+          const float* fv = reinterpret_cast<const float*>(&rv[u]);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) dst[u * RW + e] = fv[e];
+        }
+      }
+    }
+    __syncthreads();
+    stamp();
+    // ---- 2. next level's gathers, the level after next's windows ----
+    if (l + 1 < a.nlev) gather(l + 1);
+    if (dwave && l + 2 < a.nlev) decode(l + 2, sC[qd].x, sC[qd].y);
+    // ---- 3. bilinear taps -> split-fp16 A operand ----
+    {
+      const int q = tid & (kQM - 1), set = __builtin_amdgcn_readfirstlane(tid / kQM);
+      const float4 w4 = sW[l & (NS - 1)][q];
+      int pofs = (A_BYTES / 4) + q * QS + 3;
+      asm volatile("" : "+v"(pofs));  // one base register: the taps' offsets fit ds_read2_b32's immediates
+      const float* p = reinterpret_cast<const float*>(smem) + pofs;
+#pragma unroll
+      for (int S = 0; S < NSLOT; ++S) {
+        if ((S & 3) != set) continue;
+        float v[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const int k = 8 * S + e;
+          v[e] = 0.f;
+          if (k < KK) {
+            const int i = k / K, j = k - (k / K) * K;
+            v[e] = bilinear4(p[j * RW + i], p[j * RW + i + 1], p[(j + 1) * RW + i], p[(j + 1) * RW + i + 1], w4);
+          }
+          asm volatile("" : "+v"(v[e]));  // the conversions below must not fold the tap's last fma
+        }
+        range_guard8(v);
+        u32x4 hw, lw;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          typedef _Float16 h2 __attribute__((ext_vector_type(2)));
+          const h2 hp = {static_cast<_Float16>(v[2 * e]), static_cast<_Float16>(v[2 * e + 1])};
+          hw[e] = __builtin_bit_cast(unsigned, hp);
+          lw[e] = split_lo_pair(hw[e], v[2 * e], v[2 * e + 1]);
+        }
+        uint8_t* row = sA + (S >> 2) * (kQM * 128) + q * 128;
+        *reinterpret_cast<u32x4*>(row + (((S & 3) ^ swz(q)) << 4)) = hw;
+        *reinterpret_cast<u32x4*>(row + (((4 + (S & 3)) ^ swz(q)) << 4)) = lw;
+      }
+    }
+    __syncthreads();
+    stamp();
+    // ---- 4. the level's MFMAs ----
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+      u32x4 (&bc)[8] = bq[(P + g) & 1];
+#pragma unroll
+      for (int sub = 0; sub < 2; ++sub) {
+        half8 ah[2], al[2];
+        const int chi = 2 * sub + hh, clo = 4 + 2 * sub + hh;
+#pragma unroll
+        for (int mt = 0; mt < 2; ++mt) {
+          const int pr = mt * 32 + r;
+          const uint8_t* row = sA + g * (kQM * 128) + pr * 128;
+          ah[mt] = *reinterpret_cast<const half8*>(row + ((chi ^ swz(pr)) << 4));
+          al[mt] = *reinterpret_cast<const half8*>(row + ((clo ^ swz(pr)) << 4));
+        }
+#pragma unroll
+        for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+          for (int nt = 0; nt < 2; ++nt) {
+            const half8 bh = __builtin_bit_cast(half8, bc[(nt * 2 + sub) * 2 + 0]);
+            const half8 bl = __builtin_bit_cast(half8, bc[(nt * 2 + sub) * 2 + 1]);
+            acc[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[mt], bl, acc[mt][nt], 0, 0, 0);
+            acc[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[mt], bh, acc[mt][nt], 0, 0, 0);
+            acc[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[mt], bh, acc[mt][nt], 0, 0, 0);
+          }
+      }
+      const int t2 = l * G + g + 2;
+      if (t2 < nlg) load_b(t2, bc);
+    }
+    stamp();
+  };
+  for (int l = 0; l < a.nlev; l += 2) {
+    body(l, std::integral_constant<int, 0>{});
+    if (l + 1 < a.nlev) body(l + 1, std::integral_constant<int, G & 1>{});
+  }
+
+  // ---- epilogue (the r04 kernel's) ----
+  __syncthreads();
+  float* sT = reinterpret_cast<float*>(smem);
+#pragma unroll
+  for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+    for (int nt = 0; nt < 2; ++nt) {
+      const int n = wn * 64 + nt * 32 + r;
+      const int pbase = mt * 32;
+#pragma unroll
+      for (int e = 0; e < 16; ++e) sT[(pbase + (e & 3) + 8 * (e >> 2) + 4 * hh) * TS + n] = acc[mt][nt][e];
+    }
+  const int n = (tid % (kN / 8)) * 8;
+  float2 sbv[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) sbv[j] = sSB[n + j];
+  __syncthreads();
+#pragma unroll
+  for (int it = 0; it < kQM * (kN / 8) / kNT; ++it) {
+    const int pl = (tid + it * kNT) / (kN / 8);
+    if (pl >= nq) continue;
+    const float4 t0 = *reinterpret_cast<const float4*>(&sT[pl * TS + n]);
+    const float4 t1 = *reinterpret_cast<const float4*>(&sT[pl * TS + n + 4]);
+    const float v[8] = {t0.x, t0.y, t0.z, t0.w, t1.x, t1.y, t1.z, t1.w};
+    float x[8];
+    float mx = 0.f;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float2 sb = sbv[j];
+      x[j] = v[j] * sb.x + sb.y;
+      x[j] = x[j] < 0.f ? 0.f : x[j];  // relu (update.py:120); NaN propagates like ATen
+      asm volatile("" : "+v"(x[j]));
+      mx = fmaxf(mx, x[j]);
+    }
+    u32x4 hw, lw;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      typedef _Float16 h2 __attribute__((ext_vector_type(2)));
+      const h2 hp = {static_cast<_Float16>(x[2 * e]), static_cast<_Float16>(x[2 * e + 1])};
+      hw[e] = __builtin_bit_cast(unsigned, hp);
+      lw[e] = split_lo_pair(hw[e], x[2 * e], x[2 * e + 1]);
+    }
+    range_guard(mx);
+    uint8_t* line = a.y + (long long)(q0 + pl) * a.yps + (n >> 5) * 128 + ((n & 31) >> 3) * 16;
+    *reinterpret_cast<u32x4*>(line) = hw;
+    *reinterpret_cast<u32x4*>(line + 64) = lw;
+  }
+  if (a.stamps != nullptr) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  stamp();
+}
+
+
+// r05 variant 7 ("quad"): variant 6 with a gather mapping that keeps each load instruction on few tile lines: lane =
+// (query qi of a group of 4, row phase uo, chunk column k), the wave's 16 queries in 4 groups, rows uo + 4m: one
+// instruction covers 4 queries x 4 consecutive window rows x 4 chunk columns (~18 lines of 128 B against ~40 for
+// variant 6's 16 queries x 1 row), rows m and m+1 of a thread differ by one tile row (one add).
+template <int R>
+__global__ __launch_bounds__(kNT, 2) void corr_convc1_quad_kernel(C1Args a) {
+  constexpr int PK = 2 * R + 2, K = 2 * R + 1, KK = K * K;
+  constexpr int NCH = (PK + 6) / 4;
+  constexpr int RW = ((4 * NCH > PK + 3) ? 4 * NCH : PK + 3) | 1;
+  constexpr int QS = ((PK * RW + 3) | 1);
+  constexpr int G = (KK + 31) / 32;
+  constexpr int NSLOT = (KK + 7) / 8;
+  constexpr int A_BYTES = G * kQM * 128;
+  constexpr int P_BYTES = kQM * QS * 4;
+  constexpr int TS = kN + 4;
+  constexpr int EPI_BYTES = kQM * TS * 4;
+  constexpr int MAIN = A_BYTES + P_BYTES;
+  constexpr int LDS_BYTES = MAIN > EPI_BYTES ? MAIN : EPI_BYTES;
+  constexpr int NS = 4;
+  constexpr unsigned SENT = 0x80000000u;  // past any workgroup's buffer (< 2^31 bytes): the load returns zeros
+  static_assert(NCH <= 4 && kNT == 4 * kQM, "thread = (query, chunk column)");
+  static_assert(3 + 4 * NCH - 1 + (PK - 1) * RW < QS, "a row's chunks stay inside the query's patch");
+  __shared__ __attribute__((aligned(16))) uint8_t smem[LDS_BYTES];
+  __shared__ float2 sSB[kN];
+  __shared__ float2 sC[kQM];
+  __shared__ int4 sO[NS][kQM];    // window origin x0, y0, (unused), dx
+  __shared__ float4 sW[NS][kQM];  // bilinear weights (nw, ne, sw, se)
+  uint8_t* sA = smem;
+  float* sP = reinterpret_cast<float*>(smem + A_BYTES);
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wn = wave;
+  const int r = lane & 31, hh = lane >> 5;
+  const int q0 = blockIdx.x * kQM;
+  const int nq = min(kQM, a.total - q0);
+  // the gather role: lane = (query of a group of 4 qi, row phase uo, chunk column gk); the wave's 16 queries in 4 groups
+  const int gk = lane & 3, uo = (lane >> 2) & 3, qi = lane >> 4;
+  constexpr int MR = (PK + 3) / 4;  // rows uo + 4m, m < MR
+  int nst = 0;
+  auto stamp = [&]() {
+    if (a.stamps != nullptr) {
+      if (tid == 0) a.stamps[(size_t)blockIdx.x * 16 + nst] = __builtin_amdgcn_s_memtime();
+      ++nst;
+    }
+  };
+  stamp();
+  auto level = [&](int l, int& Hl, int& Wl, int& WB, int& LF, const float*& base) {
+    Hl = a.Hl[0]; Wl = a.Wl[0]; WB = a.WB[0]; LF = a.LF[0]; base = a.lv[0];
+#pragma unroll
+    for (int j = 1; j < OFLOW_MAX_LEVELS; ++j)
+      if (j == l) { Hl = a.Hl[j]; Wl = a.Wl[j]; WB = a.WB[j]; LF = a.LF[j]; base = a.lv[j]; }
+  };
+  const int qd = tid & (kQM - 1);
+  const bool dwave = tid >= (kNT - kQM);
+  auto decode = [&](int l, float cx, float cy) {
+    int xs, ys;
+    float4 w4;
+    window_origin(cx, cy, __int_as_float((127 - l) << 23), R, xs, ys, w4);  // 1/2^l exactly (corr.py:68)
+    sO[l & (NS - 1)][qd] = make_int4(xs, ys, 0, xs & 3);
+    sW[l & (NS - 1)][qd] = w4;
+  };
+
+  for (int c = tid; c < kN; c += kNT) sSB[c] = make_float2(a.wsc[c], a.bias ? a.bias[c] : 0.f);
+  if (wave < 2) {
+    float2 c = make_float2(1e30f, 1e30f);  // past the last query: all-zero window
+    if (qd < nq) {
+      const int q = q0 + qd;
+      const int b = q / a.N, pix = q - b * a.N;
+      c = make_float2(a.coords[(size_t)(2 * b) * a.N + pix], a.coords[(size_t)(2 * b + 1) * a.N + pix]);
+    }
+    if (wave == 0) sC[qd] = c;
+    if (wave < a.nlev) decode(wave, c.x, c.y);
+  }
+  for (int e = tid; e < A_BYTES / 16; e += kNT) reinterpret_cast<u32x4*>(sA)[e] = u32x4{0u, 0u, 0u, 0u};
+  __syncthreads();
+
+  u32x4 rv[4][MR];
+  auto gather = [&](int l) {
+    int Hl, Wl, WB, LF;
+    const float* base;
+    level(l, Hl, Wl, WB, LF, base);
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<float*>(base + (size_t)q0 * LF), (short)0, nq * LF * 4, 0x00020000);
+    if (NCH == 4 || gk < NCH) {
+      const int WB128 = WB * 128;
+#pragma unroll
+      for (int qq = 0; qq < 4; ++qq) {
+        const int gq = wave * 16 + qq * 4 + qi;
+        const int4 o = sO[l & (NS - 1)][gq];
+        const int xc = o.x - o.w + 4 * gk;
+        const bool cv = static_cast<unsigned>(xc) < static_cast<unsigned>(Wl) && 4 * gk < o.w + PK;
+        const int y0 = o.y + uo;
+        unsigned off = cv ? static_cast<unsigned>(__umul24(gq, LF) * 4 + ((xc >> 3) << 7) + ((xc & 7) << 2)) : SENT;
+        off += static_cast<unsigned>(__mul24(y0 >> 2, WB128) + ((y0 & 3) << 5));
+#pragma unroll
+        for (int m = 0; m < MR; ++m) {
+          if (PK % 4 == 0 || m < MR - 1 || uo + 4 * m < PK) {
+            const int y = y0 + 4 * m;
+            const unsigned o2 = static_cast<unsigned>(y) < static_cast<unsigned>(Hl) ? off + m * WB128 : SENT;
+            rv[qq][m] = __builtin_amdgcn_raw_buffer_load_b128(rs, static_cast<int>(o2), 0, 0);
+          }
+        }
+      }
+    }
+  };
+  const __amdgpu_buffer_rsrc_t rsW =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(a.wf), (short)0, a.nlev * G * kN * 128, 0x00020000);
+  const int wbase = wn * 8192 + lane * 16;
+  u32x4 bq[2][8];
+  auto load_b = [&](int t, u32x4 (&dst)[8]) {
+    const int so = t * (kN * 128);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) dst[e] = __builtin_amdgcn_raw_buffer_load_b128(rsW, wbase, so + e * 1024, 0);
+  };
+  f32x16 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
+
+  const int nlg = a.nlev * G;
+  load_b(0, bq[0]);
+  if (nlg > 1) load_b(1, bq[1]);
+  gather(0);
+  stamp();
+  auto body = [&](int l, auto Pc) {
+    constexpr int P = decltype(Pc)::value;
+    // ---- 1. chunks -> LDS patches ----
+    if (NCH == 4 || gk < NCH) {
+      int Hl, Wl, WB, LF;
+      const float* base;
+      level(l, Hl, Wl, WB, LF, base);
+#pragma unroll
+      for (int qq = 0; qq < 4; ++qq) {
+        const int gq = wave * 16 + qq * 4 + qi;
+        const int4 o = sO[l & (NS - 1)][gq];
+        int dofs = (A_BYTES / 4) + gq * QS + 3 - o.w + 4 * gk + uo * RW;
+        asm volatile("" : "+v"(dofs));  // one base register, immediate offsets
+        float* dst = reinterpret_cast<float*>(smem) + dofs;
+        const int nv = (Wl & 3) ? Wl - (o.x - o.w + 4 * gk) : 4;  // the chunk column crossing a ragged right edge
+#pragma unroll
+        for (int m = 0; m < MR; ++m) {
+          if (PK % 4 == 0 || m < MR - 1 || uo + 4 * m < PK) {
+            const float* fv = reinterpret_cast<const float*>(&rv[qq][m]);
+            if (Wl & 3) {
+              dst[4 * m * RW + 0] = fv[0];
+              dst[4 * m * RW + 1] = nv > 1 ? fv[1] : 0.f;
+              dst[4 * m * RW + 2] = nv > 2 ? fv[2] : 0.f;
+              dst[4 * m * RW + 3] = nv > 3 ? fv[3] : 0.f;
+            } else {
+#pragma unroll
+              for (int e = 0; e < 4; ++e) dst[4 * m * RW + e] = fv[e];
+            }
+          }
+        }
+      }
+    }
+    __syncthreads();
+    stamp();
+    // ---- 2. next level's gathers, the level after next's windows ----
+    if (l + 1 < a.nlev) gather(l + 1);
+    if (dwave && l + 2 < a.nlev) decode(l + 2, sC[qd].x, sC[qd].y);
+    // ---- 3. bilinear taps -> split-fp16 A operand ----
+    {
+      const int q = tid & (kQM - 1), set = __builtin_amdgcn_readfirstlane(tid / kQM);
+      const float4 w4 = sW[l & (NS - 1)][q];
+      int pofs = (A_BYTES / 4) + q * QS + 3;
+      asm volatile("" : "+v"(pofs));  // one base register: the taps' offsets fit ds_read2_b32's immediates
+      const float* p = reinterpret_cast<const float*>(smem) + pofs;
+#pragma unroll
+      for (int S = 0; S < NSLOT; ++S) {
+        if ((S & 3) != set) continue;
+        float v[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const int k = 8 * S + e;
+          v[e] = 0.f;
+          if (k < KK) {
+            const int i = k / K, j = k - (k / K) * K;
+            v[e] = bilinear4(p[j * RW + i], p[j * RW + i + 1], p[(j + 1) * RW + i], p[(j + 1) * RW + i + 1], w4);
+          }
+          asm volatile("" : "+v"(v[e]));  // the conversions below must not fold the tap's last fma
+        }
+        range_guard8(v);
+        u32x4 hw, lw;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          typedef _Float16 h2 __attribute__((ext_vector_type(2)));
+          const h2 hp = {static_cast<_Float16>(v[2 * e]), static_cast<_Float16>(v[2 * e + 1])};
+          hw[e] = __builtin_bit_cast(unsigned, hp);
+          lw[e] = split_lo_pair(hw[e], v[2 * e], v[2 * e + 1]);
+        }
+        uint8_t* row = sA + (S >> 2) * (kQM * 128) + q * 128;
+        *reinterpret_cast<u32x4*>(row + (((S & 3) ^ swz(q)) << 4)) = hw;
+        *reinterpret_cast<u32x4*>(row + (((4 + (S & 3)) ^ swz(q)) << 4)) = lw;
+      }
+    }
+    __syncthreads();
+    stamp();
+    // ---- 4. the level's MFMAs ----
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+      u32x4 (&bc)[8] = bq[(P + g) & 1];
+#pragma unroll
+      for (int sub = 0; sub < 2; ++sub) {
+        half8 ah[2], al[2];
+        const int chi = 2 * sub + hh, clo = 4 + 2 * sub + hh;
+#pragma unroll
+        for (int mt = 0; mt < 2; ++mt) {
+          const int pr = mt * 32 + r;
+          const uint8_t* row = sA + g * (kQM * 128) + pr * 128;
+          ah[mt] = *reinterpret_cast<const half8*>(row + ((chi ^ swz(pr)) << 4));
+          al[mt] = *reinterpret_cast<const half8*>(row + ((clo ^ swz(pr)) << 4));
+        }
+#pragma unroll
+        for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+          for (int nt = 0; nt < 2; ++nt) {
+            const half8 bh = __builtin_bit_cast(half8, bc[(nt * 2 + sub) * 2 + 0]);
+            const half8 bl = __builtin_bit_cast(half8, bc[(nt * 2 + sub) * 2 + 1]);
+            acc[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[mt], bl, acc[mt][nt], 0, 0, 0);
+            acc[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[mt], bh, acc[mt][nt], 0, 0, 0);
+            acc[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[mt], bh, acc[mt][nt], 0, 0, 0);
+          }
+      }
+      const int t2 = l * G + g + 2;
+      if (t2 < nlg) load_b(t2, bc);
+    }
+    stamp();
+  };
+  for (int l = 0; l < a.nlev; l += 2) {
+    body(l, std::integral_constant<int, 0>{});
+    if (l + 1 < a.nlev) body(l + 1, std::integral_constant<int, G & 1>{});
+  }
+
+  // ---- epilogue (the r04 kernel's) ----
+  __syncthreads();
+  float* sT = reinterpret_cast<float*>(smem);
+#pragma unroll
+  for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+    for (int nt = 0; nt < 2; ++nt) {
+      const int n = wn * 64 + nt * 32 + r;
+      const int pbase = mt * 32;
+#pragma unroll
+      for (int e = 0; e < 16; ++e) sT[(pbase + (e & 3) + 8 * (e >> 2) + 4 * hh) * TS + n] = acc[mt][nt][e];
+    }
+  const int n = (tid % (kN / 8)) * 8;
+  float2 sbv[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) sbv[j] = sSB[n + j];
+  __syncthreads();
+#pragma unroll
+  for (int it = 0; it < kQM * (kN / 8) / kNT; ++it) {
+    const int pl = (tid + it * kNT) / (kN / 8);
+    if (pl >= nq) continue;
+    const float4 t0 = *reinterpret_cast<const float4*>(&sT[pl * TS + n]);
+    const float4 t1 = *reinterpret_cast<const float4*>(&sT[pl * TS + n + 4]);
+    const float v[8] = {t0.x, t0.y, t0.z, t0.w, t1.x, t1.y, t1.z, t1.w};
+    float x[8];
+    float mx = 0.f;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float2 sb = sbv[j];
+      x[j] = v[j] * sb.x + sb.y;
+      x[j] = x[j] < 0.f ? 0.f : x[j];  // relu (update.py:120); NaN propagates like ATen
+      asm volatile("" : "+v"(x[j]));
+      mx = fmaxf(mx, x[j]);
+    }
+    u32x4 hw, lw;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      typedef _Float16 h2 __attribute__((ext_vector_type(2)));
+      const h2 hp = {static_cast<_Float16>(x[2 * e]), static_cast<_Float16>(x[2 * e + 1])};
+      hw[e] = __builtin_bit_cast(unsigned, hp);
+      lw[e] = split_lo_pair(hw[e], x[2 * e], x[2 * e + 1]);
+    }
+    range_guard(mx);
+    uint8_t* line = a.y + (long long)(q0 + pl) * a.yps + (n >> 5) * 128 + ((n & 31) >> 3) * 16;
+    *reinterpret_cast<u32x4*>(line) = hw;
+    *reinterpret_cast<u32x4*>(line + 64) = lw;
+  }
+  if (a.stamps != nullptr) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  stamp();
+}
+
+// r05 variant 8 ("q128"): variant 7 on 128 queries per workgroup (8 waves, one workgroup per CU), each wave 32 output
+// channels x all 128 queries (4 m tiles). PMC of the product kernel (profiles/r05/s14_pmc_c1.json): 70 % of its
+// vector-memory instructions and ~69 % of its L1->L2 requests are the weight stream (every 64-query workgroup reads
+// all 384 KB of convc1's packed weights), and the texture data path is busy 63 % of the kernel; 128 queries per
+// workgroup halve the weight stream per query. LDS 154 KB (patches 88.6 + taps 48 + tables 19), epilogue tile
+// overlaid. Same products in the same order per accumulator: bit-identical.
+template <int R>
+__global__ __launch_bounds__(512, 1) void corr_convc1_q128_kernel(C1Args a) {
+  constexpr int kNT = 512, kQM = 128;  // 8 waves, 128 queries, one workgroup per CU
+  constexpr int PK = 2 * R + 2, K = 2 * R + 1, KK = K * K;
+  constexpr int NCH = (PK + 6) / 4;
+  constexpr int RW = ((4 * NCH > PK + 3) ? 4 * NCH : PK + 3) | 1;
+  constexpr int QS = ((PK * RW + 3) | 1);
+  constexpr int G = (KK + 31) / 32;
+  constexpr int NSLOT = (KK + 7) / 8;
+  constexpr int A_BYTES = G * kQM * 128;
+  constexpr int P_BYTES = kQM * QS * 4;
+  constexpr int TS = kN + 4;
+  constexpr int EPI_BYTES = kQM * TS * 4;
+  constexpr int MAIN = A_BYTES + P_BYTES;
+  constexpr int LDS_BYTES = MAIN > EPI_BYTES ? MAIN : EPI_BYTES;
+  constexpr int NS = 4;
+  constexpr unsigned SENT = 0x80000000u;  // past any workgroup's buffer (< 2^31 bytes): the load returns zeros
+  static_assert(NCH <= 4, "chunk columns");
+  static_assert(3 + 4 * NCH - 1 + (PK - 1) * RW < QS, "a row's chunks stay inside the query's patch");
+  __shared__ __attribute__((aligned(16))) uint8_t smem[LDS_BYTES];
+  __shared__ float2 sSB[kN];
+  __shared__ float2 sC[kQM];
+  __shared__ int4 sO[NS][kQM];    // window origin x0, y0, (unused), dx
+  __shared__ float4 sW[NS][kQM];  // bilinear weights (nw, ne, sw, se)
+  uint8_t* sA = smem;
+  float* sP = reinterpret_cast<float*>(smem + A_BYTES);
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int r = lane & 31, hh = lane >> 5;
+  const int q0 = blockIdx.x * kQM;
+  const int nq = min(kQM, a.total - q0);
+  // the gather role: lane = (query of a group of 4 qi, row phase uo, chunk column gk); the wave's 16 queries in 4 groups
+  const int gk = lane & 3, uo = (lane >> 2) & 3, qi = lane >> 4;
+  constexpr int MR = (PK + 3) / 4;  // rows uo + 4m, m < MR
+  int nst = 0;
+  auto stamp = [&]() {
+    if (a.stamps != nullptr) {
+      if (tid == 0) a.stamps[(size_t)blockIdx.x * 16 + nst] = __builtin_amdgcn_s_memtime();
+      ++nst;
+    }
+  };
+  stamp();
+  auto level = [&](int l, int& Hl, int& Wl, int& WB, int& LF, const float*& base) {
+    Hl = a.Hl[0]; Wl = a.Wl[0]; WB = a.WB[0]; LF = a.LF[0]; base = a.lv[0];
+#pragma unroll
+    for (int j = 1; j < OFLOW_MAX_LEVELS; ++j)
+      if (j == l) { Hl = a.Hl[j]; Wl = a.Wl[j]; WB = a.WB[j]; LF = a.LF[j]; base = a.lv[j]; }
+  };
+  const int qd = tid & (kQM - 1);
+  const bool dwave = tid >= (kNT - kQM);
+  auto decode = [&](int l, float cx, float cy) {
+    int xs, ys;
+    float4 w4;
+    window_origin(cx, cy, __int_as_float((127 - l) << 23), R, xs, ys, w4);  // 1/2^l exactly (corr.py:68)
+    sO[l & (NS - 1)][qd] = make_int4(xs, ys, 0, xs & 3);
+    sW[l & (NS - 1)][qd] = w4;
+  };
+
+  for (int c = tid; c < kN; c += kNT) sSB[c] = make_float2(a.wsc[c], a.bias ? a.bias[c] : 0.f);
+  if (tid < 2 * kQM) {  // threads 0-127 decode level 0, 128-255 level 1
+    float2 c = make_float2(1e30f, 1e30f);  // past the last query: all-zero window
+    if (qd < nq) {
+      const int q = q0 + qd;
+      const int b = q / a.N, pix = q - b * a.N;
+      c = make_float2(a.coords[(size_t)(2 * b) * a.N + pix], a.coords[(size_t)(2 * b + 1) * a.N + pix]);
+    }
+    if (tid < kQM) sC[qd] = c;
+    if ((tid >> 7) < a.nlev) decode(tid >> 7, c.x, c.y);
+  }
+  for (int e = tid; e < A_BYTES / 16; e += kNT) reinterpret_cast<u32x4*>(sA)[e] = u32x4{0u, 0u, 0u, 0u};
+  __syncthreads();
+
+  u32x4 rv[4][MR];
+  auto gather = [&](int l) {
+    int Hl, Wl, WB, LF;
+    const float* base;
+    level(l, Hl, Wl, WB, LF, base);
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<float*>(base + (size_t)q0 * LF), (short)0, nq * LF * 4, 0x00020000);
+    if (NCH == 4 || gk < NCH) {
+      const int WB128 = WB * 128;
+#pragma unroll
+      for (int qq = 0; qq < 4; ++qq) {
+        const int gq = wave * 16 + qq * 4 + qi;
+        const int4 o = sO[l & (NS - 1)][gq];
+        const int xc = o.x - o.w + 4 * gk;
+        const bool cv = static_cast<unsigned>(xc) < static_cast<unsigned>(Wl) && 4 * gk < o.w + PK;
+        const int y0 = o.y + uo;
+        unsigned off = cv ? static_cast<unsigned>(__umul24(gq, LF) * 4 + ((xc >> 3) << 7) + ((xc & 7) << 2)) : SENT;
+        off += static_cast<unsigned>(__mul24(y0 >> 2, WB128) + ((y0 & 3) << 5));
+#pragma unroll
+        for (int m = 0; m < MR; ++m) {
+          if (PK % 4 == 0 || m < MR - 1 || uo + 4 * m < PK) {
+            const int y = y0 + 4 * m;
+            const unsigned o2 = static_cast<unsigned>(y) < static_cast<unsigned>(Hl) ? off + m * WB128 : SENT;
+            rv[qq][m] = __builtin_amdgcn_raw_buffer_load_b128(rs, static_cast<int>(o2), 0, 0);
+          }
+        }
+      }
+    }
+  };
+  const __amdgpu_buffer_rsrc_t rsW =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(a.wf), (short)0, a.nlev * G * kN * 128, 0x00020000);
+  const int wbase = wave * 4096 + lane * 16;  // wave = 32 channels = (64-channel quarter wave / 2, n tile wave & 1)
+  u32x4 bq[2][4];
+  auto load_b = [&](int t, u32x4 (&dst)[4]) {
+    const int so = t * (kN * 128);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) dst[e] = __builtin_amdgcn_raw_buffer_load_b128(rsW, wbase, so + e * 1024, 0);
+  };
+  f32x16 acc[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int e = 0; e < 16; ++e) acc[i][e] = 0.f;
+
+  const int nlg = a.nlev * G;
+  load_b(0, bq[0]);
+  if (nlg > 1) load_b(1, bq[1]);
+  gather(0);
+  stamp();
+  auto body = [&](int l, auto Pc) {
+    constexpr int P = decltype(Pc)::value;
+    // ---- 1. chunks -> LDS patches ----
+    if (NCH == 4 || gk < NCH) {
+      int Hl, Wl, WB, LF;
+      const float* base;
+      level(l, Hl, Wl, WB, LF, base);
+#pragma unroll
+      for (int qq = 0; qq < 4; ++qq) {
+        const int gq = wave * 16 + qq * 4 + qi;
+        const int4 o = sO[l & (NS - 1)][gq];
+        int dofs = (A_BYTES / 4) + gq * QS + 3 - o.w + 4 * gk + uo * RW;
+        asm volatile("" : "+v"(dofs));  // one base register, immediate offsets
+        float* dst = reinterpret_cast<float*>(smem) + dofs;
+        const int nv = (Wl & 3) ? Wl - (o.x - o.w + 4 * gk) : 4;  // the chunk column crossing a ragged right edge
+#pragma unroll
+        for (int m = 0; m < MR; ++m) {
+          if (PK % 4 == 0 || m < MR - 1 || uo + 4 * m < PK) {
+            const float* fv = reinterpret_cast<const float*>(&rv[qq][m]);
+            if (Wl & 3) {
+              dst[4 * m * RW + 0] = fv[0];
+              dst[4 * m * RW + 1] = nv > 1 ? fv[1] : 0.f;
+              dst[4 * m * RW + 2] = nv > 2 ? fv[2] : 0.f;
+              dst[4 * m * RW + 3] = nv > 3 ? fv[3] : 0.f;
+            } else {
+#pragma unroll
+              for (int e = 0; e < 4; ++e) dst[4 * m * RW + e] = fv[e];
+            }
+          }
+        }
+      }
+    }
+    __syncthreads();
+    stamp();
+    // ---- 2. next level's gathers, the level after next's windows ----
+    if (l + 1 < a.nlev) gather(l + 1);
+    if (dwave && l + 2 < a.nlev) decode(l + 2, sC[qd].x, sC[qd].y);
+    // ---- 3. bilinear taps -> split-fp16 A operand ----
+    {
+      const int q = tid & (kQM - 1), set = __builtin_amdgcn_readfirstlane(tid / kQM);
+      const float4 w4 = sW[l & (NS - 1)][q];
+      int pofs = (A_BYTES / 4) + q * QS + 3;
+      asm volatile("" : "+v"(pofs));  // one base register: the taps' offsets fit ds_read2_b32's immediates
+      const float* p = reinterpret_cast<const float*>(smem) + pofs;
+#pragma unroll
+      for (int S = 0; S < NSLOT; ++S) {
+        if ((S & 3) != set) continue;
+        float v[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const int k = 8 * S + e;
+          v[e] = 0.f;
+          if (k < KK) {
+            const int i = k / K, j = k - (k / K) * K;
+            v[e] = bilinear4(p[j * RW + i], p[j * RW + i + 1], p[(j + 1) * RW + i], p[(j + 1) * RW + i + 1], w4);
+          }
+          asm volatile("" : "+v"(v[e]));  // the conversions below must not fold the tap's last fma
+        }
+        range_guard8(v);
+        u32x4 hw, lw;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          typedef _Float16 h2 __attribute__((ext_vector_type(2)));
+          const h2 hp = {static_cast<_Float16>(v[2 * e]), static_cast<_Float16>(v[2 * e + 1])};
+          hw[e] = __builtin_bit_cast(unsigned, hp);
+          lw[e] = split_lo_pair(hw[e], v[2 * e], v[2 * e + 1]);
+        }
+        uint8_t* row = sA + (S >> 2) * (kQM * 128) + q * 128;
+        *reinterpret_cast<u32x4*>(row + (((S & 3) ^ swz(q)) << 4)) = hw;
+        *reinterpret_cast<u32x4*>(row + (((4 + (S & 3)) ^ swz(q)) << 4)) = lw;
+      }
+    }
+    __syncthreads();
+    stamp();
+    // ---- 4. the level's MFMAs ----
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+      u32x4 (&bc)[4] = bq[(P + g) & 1];
+#pragma unroll
+      for (int sub = 0; sub < 2; ++sub) {
+        half8 ah[4], al[4];
+        const int chi = 2 * sub + hh, clo = 4 + 2 * sub + hh;
+#pragma unroll
+        for (int mt = 0; mt < 4; ++mt) {
+          const int pr = mt * 32 + r;
+          const uint8_t* row = sA + g * (kQM * 128) + pr * 128;
+          ah[mt] = *reinterpret_cast<const half8*>(row + ((chi ^ swz(pr)) << 4));
+          al[mt] = *reinterpret_cast<const half8*>(row + ((clo ^ swz(pr)) << 4));
+        }
+        const half8 bh = __builtin_bit_cast(half8, bc[sub * 2 + 0]);
+        const half8 bl = __builtin_bit_cast(half8, bc[sub * 2 + 1]);
+#pragma unroll
+        for (int mt = 0; mt < 4; ++mt) {
+          acc[mt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[mt], bl, acc[mt], 0, 0, 0);
+          acc[mt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[mt], bh, acc[mt], 0, 0, 0);
+          acc[mt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[mt], bh, acc[mt], 0, 0, 0);
+        }
+      }
+      const int t2 = l * G + g + 2;
+      if (t2 < nlg) load_b(t2, bc);
+    }
+    stamp();
+  };
+  for (int l = 0; l < a.nlev; l += 2) {
+    body(l, std::integral_constant<int, 0>{});
+    if (l + 1 < a.nlev) body(l + 1, std::integral_constant<int, G & 1>{});
+  }
+
+  // ---- epilogue (the r04 kernel's) ----
+  __syncthreads();
+  float* sT = reinterpret_cast<float*>(smem);
+#pragma unroll
+  for (int mt = 0; mt < 4; ++mt) {
+    const int n = wave * 32 + r;
+    const int pbase = mt * 32;
+#pragma unroll
+    for (int e = 0; e < 16; ++e) sT[(pbase + (e & 3) + 8 * (e >> 2) + 4 * hh) * TS + n] = acc[mt][e];
+  }
+  const int n = (tid % (kN / 8)) * 8;
+  float2 sbv[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) sbv[j] = sSB[n + j];
+  __syncthreads();
+#pragma unroll
+  for (int it = 0; it < kQM * (kN / 8) / kNT; ++it) {
+    const int pl = (tid + it * kNT) / (kN / 8);
+    if (pl >= nq) continue;
+    const float4 t0 = *reinterpret_cast<const float4*>(&sT[pl * TS + n]);
+    const float4 t1 = *reinterpret_cast<const float4*>(&sT[pl * TS + n + 4]);
+    const float v[8] = {t0.x, t0.y, t0.z, t0.w, t1.x, t1.y, t1.z, t1.w};
+    float x[8];
+    float mx = 0.f;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float2 sb = sbv[j];
+      x[j] = v[j] * sb.x + sb.y;
+      x[j] = x[j] < 0.f ? 0.f : x[j];  // relu (update.py:120); NaN propagates like ATen
+      asm volatile("" : "+v"(x[j]));
+      mx = fmaxf(mx, x[j]);
+    }
+    u32x4 hw, lw;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      typedef _Float16 h2 __attribute__((ext_vector_type(2)));
+      const h2 hp = {static_cast<_Float16>(x[2 * e]), static_cast<_Float16>(x[2 * e + 1])};
+      hw[e] = __builtin_bit_cast(unsigned, hp);
+      lw[e] = split_lo_pair(hw[e], x[2 * e], x[2 * e + 1]);
+    }
+    range_guard(mx);
+    uint8_t* line = a.y + (long long)(q0 + pl) * a.yps + (n >> 5) * 128 + ((n & 31) >> 3) * 16;
+    *reinterpret_cast<u32x4*>(line) = hw;
+    *reinterpret_cast<u32x4*>(line + 64) = lw;
+  }
+  if (a.stamps != nullptr) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  stamp();
+}
+
 }  // namespace
+// keeps the range guards' flag pointer (and so their code) alive, as in the product library
+OFLOW_RANGE_FLAG_SETTER(c1var)
 }  // namespace oflow
 
 using namespace oflow;
@@ -1329,6 +2190,12 @@ extern "C" int oflow_exp_convc1_variant(int variant, const float* const* d_level
     case 43: hipLaunchKernelGGL((corr_convc1_lean_kernel<3>), grid, dim3(256), 0, s, a); break;
     case 54: hipLaunchKernelGGL((corr_convc1_hyb_kernel<4>), grid, dim3(256), 0, s, a); break;
     case 53: hipLaunchKernelGGL((corr_convc1_hyb_kernel<3>), grid, dim3(256), 0, s, a); break;
+    case 64: hipLaunchKernelGGL((corr_convc1_rowmap_kernel<4>), grid, dim3(256), 0, s, a); break;
+    case 63: hipLaunchKernelGGL((corr_convc1_rowmap_kernel<3>), grid, dim3(256), 0, s, a); break;
+    case 74: hipLaunchKernelGGL((corr_convc1_quad_kernel<4>), grid, dim3(256), 0, s, a); break;
+    case 73: hipLaunchKernelGGL((corr_convc1_quad_kernel<3>), grid, dim3(256), 0, s, a); break;
+    case 84: hipLaunchKernelGGL((corr_convc1_q128_kernel<4>), dim3((a.total + 127) / 128), dim3(512), 0, s, a); break;
+    case 83: hipLaunchKernelGGL((corr_convc1_q128_kernel<3>), dim3((a.total + 127) / 128), dim3(512), 0, s, a); break;
     default: return OFLOW_E_MODE;
   }
   return launch_status();

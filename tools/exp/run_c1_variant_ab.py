@@ -20,7 +20,7 @@ from model import synthetic  # noqa: E402
 from model.utils import coords_grid  # noqa: E402
 
 DEV = torch.device("cuda", 0)
-VARIANTS = [int(v) for v in os.environ.get("VARIANTS", "1,2,3,4,5").split(",")]
+VARIANTS = [int(v) for v in os.environ.get("VARIANTS", "1,2,3,4,5,6").split(",")]
 
 
 def timeit(fn, reps=20, burst=5):
@@ -72,13 +72,30 @@ def s32_values(y):
     return (v[:, :, 0] + v[:, :, 1]).reshape(y.shape[0], -1)
 
 
+def check_shape(cw, b, h, w):
+    """bit-identity of every variant with variant 1 on one more grid (e.g. KITTI's 47x156: levels 39 and 19 px wide,
+    whose right-edge chunk columns cross the level's edge)"""
+    f1, f2 = synthetic.synthetic_fmaps(b, 256, h, w, stream=5)
+    pyr = N.corr_pyramid_tiled(f1.to(DEV), f2.to(DEV), 4)
+    coords = (coords_grid(b, h, w) + torch.from_numpy(synthetic.hash_normal(11, (b, 2, h, w), 6.0))).to(DEV).contiguous()
+    vcall = variant_caller(N, cw, coords, b, h, w)
+    ys = {}
+    with torch.inference_mode():
+        for v in VARIANTS:
+            ys[v] = N.s32_empty(b, h, w, 8, DEV)
+            ys[v].fill_(0)
+            vcall(v, pyr, ys[v])
+        torch.cuda.synchronize()
+    return {f"v{v}": bool(torch.equal(ys[v], ys[VARIANTS[0]])) for v in VARIANTS[1:]}
+
+
 def main():
     h, w = 55, 128
     conv = torch.nn.Conv2d(324, 256, 1).to(DEV)
     with torch.no_grad():
         conv.weight.mul_(4.0)
     cw = N.convc1_level_weights(conv, 4, 4)
-    out = {}
+    out = {"kitti47x156_bit_identical": check_shape(cw, 2, 47, 156)}
     for b in (8, 4):
         pyrs = []
         for k in range(3):

@@ -60,28 +60,36 @@ constexpr bool magic16_ok(unsigned d, unsigned lim) {
 }
 
 // Per workgroup (64 queries, 4 waves; wave w = output channels 64w..64w+63), level by level:
-//   * gathers: a window row of PK cells starting at x0 lies inside NCH 16-B aligned chunks from xa = x0 & ~3 (a chunk
-//     never crosses a 4x8 tile: tile rows are 32 B), one buffer_load_dwordx4 per chunk; per-(query, level) window
-//     origin and row / column validity masks come from LDS (decoded two levels ahead), offsets are branch-free (a chunk
-//     not needed loads the workgroup's first 16 B);
+//   * gathers: lane = (query qi of a group of 4, row phase uo, chunk column k); a wave covers its 16 queries in 4
+//     groups, rows uo + 4m, so one buffer_load_dwordx4 instruction reads 4 queries x 4 consecutive window rows x 4
+//     16-B chunk columns (a chunk never crosses a 4x8 tile: tile rows are 32 B; ~18 lines of 128 B per instruction).
+//     A chunk column's byte offset (query base folded in) is formed once per (query, level), or set to a sentinel past
+//     the buffer when the column lies outside the level or the window; each row adds its tile-row part (rows m and
+//     m+1 are one tile row apart: one add) and takes the sentinel when outside the level. A sentinel load returns
+//     zeros without a memory access: the zero padding of Q4.
 //   * patches in LDS: row u of query q at sP[q*QS + u*RW], the window's cells at +3 .. +3+PK-1; a chunk's 4 floats go
-//     to +3 + 4k + e - dx (dx = x0 - xa), the ones outside the window into the row's slack (RW >= 4*NCH: never another
-//     row's cells); cells outside the level (zero padding, Q4) are written as 0 from the masks;
+//     to +3 + 4k + e - dx (dx = x0 & 3) by four ds_write_b32 at immediate offsets from one per-(query, level) base; the
+//     chunks of a row cover disjoint cells, the ones outside the window land in the row's slack (RW >= 4*NCH, the
+//     last one at most 2 floats into the next row's slack). A level whose width is not a multiple of 4 masks the cells
+//     of the one chunk column crossing its right edge (tile padding).
 //   * level l+1's gathers are issued right after level l's patches are in LDS, so they fly during level l's taps and
 //     MFMAs;
+//   * taps: bilinear4 per tap, hi by v_cvt_pk_f16_f32 (two taps, RNE), lo = fp16(v - hi) by v_fma_mixlo/mixhi_f16
+//     (split_lo_pair: v - hi is exact in fp32, so the one rounding equals the cvt(sub) pair's);
 //   * B (weights, fragment-major: one wave instruction = 1 KB contiguous, L2-resident) goes straight into the MFMA
 //     operand registers through a 2-deep ring of k32 groups, each group's load issued right after the MFMAs of the
 //     group two before it. Vector-memory loads retire in issue order, so only a group whose load follows the next
 //     level's gathers waits for them (G = 3: the level's last group).
-// Taps, split and MFMA order are those of the round-2 kernel (LDS-staged weights, dword gathers; git history and
-// tools/build_rev.sh for A/B): the output is bit for bit the same.
+// r05 (tools/exp/corr_convc1_variants.hip variant 7, profiles/r05/s13-s14): the r04 kernel's chunk items were decoded
+// per item (query, row, chunk) with per-element masks and selects -- ~680 of 1,190 VALU per wave and level; this
+// mapping and the mix split take the static VALU count from 4,471 to ~2,590, 37.2 -> 35.8 us per 4-pair launch alone.
+// Taps, split values, MFMA order and epilogue are unchanged: bit for bit the r04 kernel's output.
 template <int R>
 __global__ __launch_bounds__(kNT, 2) void corr_convc1_kernel(C1Args a) {
   constexpr int PK = 2 * R + 2, K = 2 * R + 1, KK = K * K;
-  constexpr int NCH = (PK + 6) / 4;                          // chunks per window row (dx <= 3)
-  constexpr int RW = ((4 * NCH > PK + 3) ? 4 * NCH : PK + 3) | 1;  // LDS row pitch (floats; odd: spreads the
-                                                                    // chunk writes of consecutive rows over banks)
-  constexpr int QS = ((PK * RW + 3) | 1);                    // per-query pitch: odd -> conflict-free tap reads
+  constexpr int NCH = (PK + 6) / 4;
+  constexpr int RW = ((4 * NCH > PK + 3) ? 4 * NCH : PK + 3) | 1;
+  constexpr int QS = ((PK * RW + 3) | 1);
   constexpr int G = (KK + 31) / 32;
   constexpr int NSLOT = (KK + 7) / 8;
   constexpr int A_BYTES = G * kQM * 128;
@@ -90,25 +98,27 @@ __global__ __launch_bounds__(kNT, 2) void corr_convc1_kernel(C1Args a) {
   constexpr int EPI_BYTES = kQM * TS * 4;
   constexpr int MAIN = A_BYTES + P_BYTES;
   constexpr int LDS_BYTES = MAIN > EPI_BYTES ? MAIN : EPI_BYTES;
-  constexpr int CITEMS = kQM * PK * NCH;                     // chunk items per level
-  constexpr int NI = (CITEMS + kNT - 1) / kNT;
-  constexpr int NS = 4;                                      // decode slots (level & 3)
-  static_assert(4 * NCH <= 16 && PK <= 16, "mask widths");
+  constexpr int NS = 4;
+  constexpr unsigned SENT = 0x80000000u;  // past any workgroup's buffer (< 2^31 bytes): the load returns zeros
+  static_assert(NCH <= 4 && kNT == 4 * kQM, "thread = (query, chunk column)");
+  static_assert(3 + 4 * NCH - 1 + (PK - 1) * RW < QS, "a row's chunks stay inside the query's patch");
   __shared__ __attribute__((aligned(16))) uint8_t smem[LDS_BYTES];
   __shared__ float2 sSB[kN];
   __shared__ float2 sC[kQM];
-  __shared__ int4 sO[NS][kQM];    // window origin x0, y0, masks (x: bits 0-15, y: bits 16-31), dx
+  __shared__ int4 sO[NS][kQM];    // window origin x0, y0, (unused), dx
   __shared__ float4 sW[NS][kQM];  // bilinear weights (nw, ne, sw, se)
-  uint8_t* sA = smem;
-  float* sP = reinterpret_cast<float*>(smem + A_BYTES);
+  uint8_t* sA = smem;  // the taps (A operand); the patches follow at float offset A_BYTES / 4
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wn = wave;
   const int r = lane & 31, hh = lane >> 5;
   const int q0 = blockIdx.x * kQM;
   const int nq = min(kQM, a.total - q0);
+  // the gather role: lane = (query of a group of 4 qi, row phase uo, chunk column gk); the wave's 16 queries in 4 groups
+  const int gk = lane & 3, uo = (lane >> 2) & 3, qi = lane >> 4;
+  constexpr int MR = (PK + 3) / 4;  // rows uo + 4m, m < MR
   int nst = 0;
-  auto stamp = [&]() {  // diagnostics (experiment hook): per-workgroup clock stamps
+  auto stamp = [&]() {
     if (a.stamps != nullptr) {
       if (tid == 0) a.stamps[(size_t)blockIdx.x * 16 + nst] = __builtin_amdgcn_s_memtime();
       ++nst;
@@ -121,28 +131,17 @@ __global__ __launch_bounds__(kNT, 2) void corr_convc1_kernel(C1Args a) {
     for (int j = 1; j < OFLOW_MAX_LEVELS; ++j)
       if (j == l) { Hl = a.Hl[j]; Wl = a.Wl[j]; WB = a.WB[j]; LF = a.LF[j]; base = a.lv[j]; }
   };
-  const int qd = tid & (kQM - 1);            // the query a decoding thread handles
-  const bool dwave = tid >= (kNT - kQM);      // wave 3: decodes levels 2.. inside the loop
-  // window of query qd at level l -> sO / sW[l & 3]
+  const int qd = tid & (kQM - 1);
+  const bool dwave = tid >= (kNT - kQM);
   auto decode = [&](int l, float cx, float cy) {
-    int Hl, Wl, WB, LF;
-    const float* base;
-    level(l, Hl, Wl, WB, LF, base);
     int xs, ys;
     float4 w4;
     window_origin(cx, cy, __int_as_float((127 - l) << 23), R, xs, ys, w4);  // 1/2^l exactly (corr.py:68)
-    const int dx = xs & 3, xa = xs - dx;
-    const int xl = max(0, -xa), xh = min(4 * NCH, Wl - xa);
-    const int yl = max(0, -ys), yh = min(PK, Hl - ys);
-    const unsigned xm = xh > xl ? (((1u << (xh - xl)) - 1u) << xl) : 0u;
-    const unsigned ym = yh > yl ? (((1u << (yh - yl)) - 1u) << yl) : 0u;
-    sO[l & (NS - 1)][qd] = make_int4(xs, ys, static_cast<int>(xm | (ym << 16)), dx);
+    sO[l & (NS - 1)][qd] = make_int4(xs, ys, 0, xs & 3);
     sW[l & (NS - 1)][qd] = w4;
   };
 
   for (int c = tid; c < kN; c += kNT) sSB[c] = make_float2(a.wsc[c], a.bias ? a.bias[c] : 0.f);
-  // the query's coordinates; waves 0 and 1 decode levels 0 and 1 (wave 3, the one with the fewest tap slots, decodes
-  // the later levels inside the loop)
   if (wave < 2) {
     float2 c = make_float2(1e30f, 1e30f);  // past the last query: all-zero window
     if (qd < nq) {
@@ -153,58 +152,42 @@ __global__ __launch_bounds__(kNT, 2) void corr_convc1_kernel(C1Args a) {
     if (wave == 0) sC[qd] = c;
     if (wave < a.nlev) decode(wave, c.x, c.y);
   }
-  // A's taps past KK (the last group's tail) are never written again: zero the whole A buffer once
   for (int e = tid; e < A_BYTES / 16; e += kNT) reinterpret_cast<u32x4*>(sA)[e] = u32x4{0u, 0u, 0u, 0u};
   __syncthreads();
-  // chunk item s of this thread -> (query, window row, chunk): recomputed per use (a few full-rate ops; no live
-  // registers across the level)
-  static_assert(magic16_ok(PK * NCH, CITEMS) && magic16_ok(NCH, PK * NCH), "chunk item decode");
-  auto item_of = [&](int s, int& q, int& u, int& k) {
-    int t_ = tid;
-    asm volatile("" : "+v"(t_));
-    const unsigned item = static_cast<unsigned>(min(t_ + kNT * s, CITEMS - 1));
-    q = static_cast<int>(__umul24(item, magic16(PK * NCH)) >> 16);
-    const unsigned rm = item - static_cast<unsigned>(q) * (PK * NCH);
-    u = static_cast<int>(__umul24(rm, magic16(NCH)) >> 16);
-    k = static_cast<int>(rm - static_cast<unsigned>(u) * NCH);
-  };
 
-  u32x4 rv[NI];
+  u32x4 rv[4][MR];
   auto gather = [&](int l) {
     int Hl, Wl, WB, LF;
     const float* base;
     level(l, Hl, Wl, WB, LF, base);
     const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
         const_cast<float*>(base + (size_t)q0 * LF), (short)0, nq * LF * 4, 0x00020000);
-    constexpr int HB = (NI + 1) / 2;  // two batches of window reads: fewer live registers
+    if (NCH == 4 || gk < NCH) {
+      const int WB128 = WB * 128;
 #pragma unroll
-    for (int s0 = 0; s0 < NI; s0 += HB) {
-      int4 o[NI];
-      int qs[NI], us[NI], ks[NI];
+      for (int qq = 0; qq < 4; ++qq) {
+        const int gq = wave * 16 + qq * 4 + qi;
+        const int4 o = sO[l & (NS - 1)][gq];
+        const int xc = o.x - o.w + 4 * gk;
+        const bool cv = static_cast<unsigned>(xc) < static_cast<unsigned>(Wl) && 4 * gk < o.w + PK;
+        const int y0 = o.y + uo;
+        unsigned off = cv ? static_cast<unsigned>(__umul24(gq, LF) * 4 + ((xc >> 3) << 7) + ((xc & 7) << 2)) : SENT;
+        off += static_cast<unsigned>(__mul24(y0 >> 2, WB128) + ((y0 & 3) << 5));
 #pragma unroll
-      for (int s = s0; s < (NI < s0 + HB ? NI : s0 + HB); ++s) {
-        item_of(s, qs[s], us[s], ks[s]);
-        o[s] = sO[l & (NS - 1)][qs[s]];
-      }
-#pragma unroll
-      for (int s = s0; s < (NI < s0 + HB ? NI : s0 + HB); ++s) {
-        const int q = qs[s], u = us[s], k = ks[s];
-        const int y = o[s].y + u, xc = (o[s].x - o[s].w) + 4 * k;
-        // the chunk holds a needed, in-level cell: row u valid, one of its 4 columns valid and inside the window
-        const unsigned need = ((static_cast<unsigned>(o[s].z) >> 16) >> u) & 1u &
-                              (((static_cast<unsigned>(o[s].z) & 0xffffu) >> (4 * k)) & 15u ? 1u : 0u) &
-                              (4 * k < o[s].w + PK ? 1u : 0u);
-        int off = (__umul24(q, LF) + (__umul24(static_cast<unsigned>(y) >> 2, WB) + (xc >> 3)) * 32 + ((y & 3) << 3) + (xc & 7)) * 4;
-        asm volatile("" : "+v"(off));  // computed unconditionally: a select, not an exec branch around it
-        off = need ? off : 0;
-        rv[s] = __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0);
+        for (int m = 0; m < MR; ++m) {
+          if (PK % 4 == 0 || m < MR - 1 || uo + 4 * m < PK) {
+            const int y = y0 + 4 * m;
+            const unsigned o2 = static_cast<unsigned>(y) < static_cast<unsigned>(Hl) ? off + m * WB128 : SENT;
+            rv[qq][m] = __builtin_amdgcn_raw_buffer_load_b128(rs, static_cast<int>(o2), 0, 0);
+          }
+        }
       }
     }
   };
   const __amdgpu_buffer_rsrc_t rsW =
       __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(a.wf), (short)0, a.nlev * G * kN * 128, 0x00020000);
   const int wbase = wn * 8192 + lane * 16;
-  u32x4 bq[2][8];  // B ring: global k32 group t in bq[t & 1]; [(nt * 2 + sub) * 2 + hi/lo]
+  u32x4 bq[2][8];
   auto load_b = [&](int t, u32x4 (&dst)[8]) {
     const int so = t * (kN * 128);
 #pragma unroll
@@ -223,67 +206,83 @@ __global__ __launch_bounds__(kNT, 2) void corr_convc1_kernel(C1Args a) {
   if (nlg > 1) load_b(1, bq[1]);
   gather(0);
   stamp();
-  // one level; P = (l * G) & 1: the ring slot of the level's first group
   auto body = [&](int l, auto Pc) {
     constexpr int P = decltype(Pc)::value;
-    // ---- 1. chunks -> LDS patches (cells outside the level zeroed) ----
+    // ---- 1. chunks -> LDS patches ----
+    if (NCH == 4 || gk < NCH) {
+      int Hl, Wl, WB, LF;
+      const float* base;
+      level(l, Hl, Wl, WB, LF, base);
 #pragma unroll
-    for (int s = 0; s < NI; ++s) {
-      if (CITEMS % kNT == 0 || tid + kNT * s < CITEMS) {
-        int q, u, k;
-        item_of(s, q, u, k);
-        const int4 o = sO[l & (NS - 1)][q];
-        const unsigned m = (((static_cast<unsigned>(o.z) >> 16) >> u) & 1u) ? ((static_cast<unsigned>(o.z) >> (4 * k)) & 15u) : 0u;
-        const float* fv = reinterpret_cast<const float*>(&rv[s]);
-        float* dst = sP + q * QS + u * RW + 3 + 4 * k - o.w;
+      for (int qq = 0; qq < 4; ++qq) {
+        const int gq = wave * 16 + qq * 4 + qi;
+        const int4 o = sO[l & (NS - 1)][gq];
+        int dofs = (A_BYTES / 4) + gq * QS + 3 - o.w + 4 * gk + uo * RW;
+        asm volatile("" : "+v"(dofs));  // one base register, immediate offsets
+        float* dst = reinterpret_cast<float*>(smem) + dofs;
+        const int nv = (Wl & 3) ? Wl - (o.x - o.w + 4 * gk) : 4;  // the chunk column crossing a ragged right edge
 #pragma unroll
-        for (int e = 0; e < 4; ++e) dst[e] = ((m >> e) & 1u) ? fv[e] : 0.0f;
+        for (int m = 0; m < MR; ++m) {
+          if (PK % 4 == 0 || m < MR - 1 || uo + 4 * m < PK) {
+            const float* fv = reinterpret_cast<const float*>(&rv[qq][m]);
+            if (Wl & 3) {
+              dst[4 * m * RW + 0] = fv[0];
+              dst[4 * m * RW + 1] = nv > 1 ? fv[1] : 0.f;
+              dst[4 * m * RW + 2] = nv > 2 ? fv[2] : 0.f;
+              dst[4 * m * RW + 3] = nv > 3 ? fv[3] : 0.f;
+            } else {
+#pragma unroll
+              for (int e = 0; e < 4; ++e) dst[4 * m * RW + e] = fv[e];
+            }
+          }
+        }
       }
     }
-    __syncthreads();  // patches complete; every wave is past level l-1's MFMAs (A free)
+    __syncthreads();
     stamp();
-    // ---- 2. next level's gathers (rv is free), the level after next's windows ----
+    // ---- 2. next level's gathers, the level after next's windows ----
     if (l + 1 < a.nlev) gather(l + 1);
     if (dwave && l + 2 < a.nlev) decode(l + 2, sC[qd].x, sC[qd].y);
-    // ---- 3. bilinear taps -> split-fp16 A operand; the slot set is the wave index (a scalar branch per slot) ----
+    // ---- 3. bilinear taps -> split-fp16 A operand ----
     {
       const int q = tid & (kQM - 1), set = __builtin_amdgcn_readfirstlane(tid / kQM);
       const float4 w4 = sW[l & (NS - 1)][q];
-      const float* p = sP + q * QS + 3;
+      int pofs = (A_BYTES / 4) + q * QS + 3;
+      asm volatile("" : "+v"(pofs));  // one base register: the taps' offsets fit ds_read2_b32's immediates
+      const float* p = reinterpret_cast<const float*>(smem) + pofs;
 #pragma unroll
       for (int S = 0; S < NSLOT; ++S) {
         if ((S & 3) != set) continue;
-        float v[8];  // all 8 taps first (the shared cells are read once), then the splits
+        float v[8];
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
-          const int k = 8 * S + e;  // reference channel order within the level: k = i*K + j, i moves x, j moves y
+          const int k = 8 * S + e;
           v[e] = 0.f;
           if (k < KK) {
             const int i = k / K, j = k - (k / K) * K;
             v[e] = bilinear4(p[j * RW + i], p[j * RW + i + 1], p[(j + 1) * RW + i], p[(j + 1) * RW + i + 1], w4);
           }
+          asm volatile("" : "+v"(v[e]));  // the conversions below must not fold the tap's last fma
         }
         range_guard8(v);
-        half8 hi, lo;
+        u32x4 hw, lw;
 #pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          _Float16 h_, l_;
-          split_f16(v[e], h_, l_);
-          hi[e] = h_;
-          lo[e] = l_;
+        for (int e = 0; e < 4; ++e) {
+          typedef _Float16 h2 __attribute__((ext_vector_type(2)));
+          const h2 hp = {static_cast<_Float16>(v[2 * e]), static_cast<_Float16>(v[2 * e + 1])};
+          hw[e] = __builtin_bit_cast(unsigned, hp);
+          lw[e] = split_lo_pair(hw[e], v[2 * e], v[2 * e + 1]);
         }
         uint8_t* row = sA + (S >> 2) * (kQM * 128) + q * 128;
-        *reinterpret_cast<half8*>(row + (((S & 3) ^ swz(q)) << 4)) = hi;
-        *reinterpret_cast<half8*>(row + (((4 + (S & 3)) ^ swz(q)) << 4)) = lo;
+        *reinterpret_cast<u32x4*>(row + (((S & 3) ^ swz(q)) << 4)) = hw;
+        *reinterpret_cast<u32x4*>(row + (((4 + (S & 3)) ^ swz(q)) << 4)) = lw;
       }
     }
-    __syncthreads();  // A complete; the patches consumed
+    __syncthreads();
     stamp();
     // ---- 4. the level's MFMAs ----
 #pragma unroll
     for (int g = 0; g < G; ++g) {
-      constexpr int dummy = 0;
-      (void)dummy;
       u32x4 (&bc)[8] = bq[(P + g) & 1];
 #pragma unroll
       for (int sub = 0; sub < 2; ++sub) {
@@ -307,18 +306,18 @@ __global__ __launch_bounds__(kNT, 2) void corr_convc1_kernel(C1Args a) {
             acc[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[mt], bh, acc[mt][nt], 0, 0, 0);
           }
       }
-      const int t2 = l * G + g + 2;  // the ring slot is free: the group two ahead
+      const int t2 = l * G + g + 2;
       if (t2 < nlg) load_b(t2, bc);
     }
     stamp();
   };
   for (int l = 0; l < a.nlev; l += 2) {
-    body(l, std::integral_constant<int, 0>{});  // (l * G) & 1 = 0 for even l
+    body(l, std::integral_constant<int, 0>{});
     if (l + 1 < a.nlev) body(l + 1, std::integral_constant<int, G & 1>{});
   }
 
-  // ---- epilogue: accumulators -> LDS tile [pixel][channel] -> scale, bias, ReLU -> S32 ----
-  __syncthreads();  // every wave is past its last A read (the tile overlays A and the patches)
+  // ---- epilogue (the r04 kernel's) ----
+  __syncthreads();
   float* sT = reinterpret_cast<float*>(smem);
 #pragma unroll
   for (int mt = 0; mt < 2; ++mt)
@@ -329,8 +328,6 @@ __global__ __launch_bounds__(kNT, 2) void corr_convc1_kernel(C1Args a) {
 #pragma unroll
       for (int e = 0; e < 16; ++e) sT[(pbase + (e & 3) + 8 * (e >> 2) + 4 * hh) * TS + n] = acc[mt][nt][e];
     }
-  // each thread's 8 channels are the same for every item (kNT is a multiple of kN / 8): their (scale, bias) once
-  static_assert(kNT % (kN / 8) == 0, "fixed channel octet per thread");
   const int n = (tid % (kN / 8)) * 8;
   float2 sbv[8];
 #pragma unroll
@@ -343,23 +340,28 @@ __global__ __launch_bounds__(kNT, 2) void corr_convc1_kernel(C1Args a) {
     const float4 t0 = *reinterpret_cast<const float4*>(&sT[pl * TS + n]);
     const float4 t1 = *reinterpret_cast<const float4*>(&sT[pl * TS + n + 4]);
     const float v[8] = {t0.x, t0.y, t0.z, t0.w, t1.x, t1.y, t1.z, t1.w};
-    half8 hi, lo;
+    float x[8];
     float mx = 0.f;
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       const float2 sb = sbv[j];
-      float x = v[j] * sb.x + sb.y;
-      x = x < 0.f ? 0.f : x;  // relu (update.py:120); NaN propagates like ATen
-      mx = fmaxf(mx, x);
-      _Float16 h_, l_;
-      split_f16(x, h_, l_);
-      hi[j] = h_;
-      lo[j] = l_;
+      x[j] = v[j] * sb.x + sb.y;
+      x[j] = x[j] < 0.f ? 0.f : x[j];  // relu (update.py:120); NaN propagates like ATen
+      asm volatile("" : "+v"(x[j]));
+      mx = fmaxf(mx, x[j]);
+    }
+    u32x4 hw, lw;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      typedef _Float16 h2 __attribute__((ext_vector_type(2)));
+      const h2 hp = {static_cast<_Float16>(x[2 * e]), static_cast<_Float16>(x[2 * e + 1])};
+      hw[e] = __builtin_bit_cast(unsigned, hp);
+      lw[e] = split_lo_pair(hw[e], x[2 * e], x[2 * e + 1]);
     }
     range_guard(mx);
     uint8_t* line = a.y + (long long)(q0 + pl) * a.yps + (n >> 5) * 128 + ((n & 31) >> 3) * 16;
-    *reinterpret_cast<half8*>(line) = hi;
-    *reinterpret_cast<half8*>(line + 64) = lo;
+    *reinterpret_cast<u32x4*>(line) = hw;
+    *reinterpret_cast<u32x4*>(line + 64) = lw;
   }
   if (a.stamps != nullptr) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   stamp();

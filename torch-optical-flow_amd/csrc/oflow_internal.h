@@ -40,6 +40,20 @@ __device__ __forceinline__ void split_f16(float v, _Float16& hi, _Float16& lo) {
   lo = static_cast<_Float16>(v - static_cast<float>(a));
 }
 
+// The lo halves of two values whose hi halves are packed in hi2 (hi2 = v_cvt_pk_f16_f32(v0, v1), RNE):
+// fp16(v0 - hi0) | fp16(v1 - hi1) << 16 by v_fma_mixlo/mixhi_f16 (-hi * 1 + v, one rounding). v - hi is exact in fp32
+// (|v - hi| <= half an fp16 ulp of v, a multiple of v's fp32 ulp), so the result equals split_f16's
+// fp16(v - fp32(hi)) bit for bit, in 2 VALU per pair instead of 6. The callers pin v to a VGPR before converting
+// (split_f16's note: a multiply producing v must not fold into the conversion).
+__device__ __forceinline__ unsigned split_lo_pair(unsigned hi2, float v0, float v1) {
+  unsigned lo;
+  asm("v_fma_mixlo_f16 %0, -%1, 1.0, %2 op_sel_hi:[1,0,0]\n\t"
+      "v_fma_mixhi_f16 %0, -%1, 1.0, %3 op_sel:[1,0,0] op_sel_hi:[1,0,0]"
+      : "=&v"(lo)
+      : "v"(hi2), "v"(v0), "v"(v1));
+  return lo;
+}
+
 // Range guard of the split-fp16 operands (S32, include/oflow.h): a value whose hi half would overflow fp16 (|v| >= 65520
 // rounds to inf; inf included, NaN not) sets the device flag registered by oflow_set_range_flag (sticky; the host reads
 // it once per forward and raises). Every translation unit that splits holds its own copy of the flag pointer
