@@ -141,15 +141,7 @@ __device__ __forceinline__ float act_fn(float v, int act) {
   return v;
 }
 
-__device__ __forceinline__ void split8(const float* v, half8& hi, half8& lo) {
-#pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    _Float16 h_, l_;
-    split_f16(v[j], h_, l_);
-    hi[j] = h_;
-    lo[j] = l_;
-  }
-}
+__device__ __forceinline__ void split8(const float* v, half8& hi, half8& lo) { split_vec(v, hi, lo); }
 
 // store channels [n, n + 8) of pixel P (n % 8 == 0) into an S32 destination, only those < N; the max |x| of the stored
 // values goes into gm (the caller range-guards once per epilogue: one branch instead of one per item)
@@ -353,19 +345,16 @@ __global__ __launch_bounds__(64 * WM * WN, WM * WN == 8 ? 1 : 2) void conv_s32_k
           const int pb_ = 2 * (p >> 5) * kImgPitch + (p & 31);                                                       \
           const int4 ko_ = *reinterpret_cast<const int4*>(sKoff + (G) * 32 + 4 * c);                                 \
           const int kov_[4] = {ko_.x, ko_.y, ko_.z, ko_.w};                                                          \
-          float mx_ = 0.f;                                                                                           \
+          float mx_ = 0.f, v4_[4];                                                                                   \
           _Pragma("unroll") for (int e_ = 0; e_ < 4; ++e_) {                                                         \
-            const float v_ = sImg[kov_[e_] < 0 ? kImgZero : pb_ + kov_[e_]];                                         \
-            mx_ = fmaxf(mx_, fabsf(v_));                                                                             \
-            _Float16 hv, lv;                                                                                         \
-            split_f16(v_, hv, lv);                                                                                   \
-            h4[e_] = hv;                                                                                             \
-            l4[e_] = lv;                                                                                             \
+            v4_[e_] = sImg[kov_[e_] < 0 ? kImgZero : pb_ + kov_[e_]];                                                \
+            mx_ = fmaxf(mx_, fabsf(v4_[e_]));                                                                        \
           }                                                                                                          \
+          split_vec(v4_, h4, l4);                                                                                    \
           amx_ = fmaxf(amx_, mx_);                                                                                   \
         } else if (((aok >> s_) & 1u) && (AIN != kInF32 || (G) * 32 + 4 * c < a.cin)) {                             \
           const float* fv = reinterpret_cast<const float*>(&RA[s_]);                                                 \
-          float mx_ = 0.f;                                                                                           \
+          float mx_ = 0.f, v4_[4];                                                                                   \
           _Pragma("unroll") for (int e_ = 0; e_ < 4; ++e_) {                                                         \
             float v_ = fv[e_];                                                                                       \
             if constexpr (AIN == kInF32Norm) {                                                                       \
@@ -374,11 +363,9 @@ __global__ __launch_bounds__(64 * WM * WN, WM * WN == 8 ? 1 : 2) void conv_s32_k
               v_ = v_ < 0.f ? 0.f : v_;                                                                              \
             }                                                                                                        \
             mx_ = fmaxf(mx_, fabsf(v_));                                                                             \
-            _Float16 hv, lv;                                                                                         \
-            split_f16(v_, hv, lv);                                                                                   \
-            h4[e_] = hv;                                                                                             \
-            l4[e_] = lv;                                                                                             \
+            v4_[e_] = v_;                                                                                            \
           }                                                                                                          \
+          split_vec(v4_, h4, l4);                                                                                    \
           amx_ = fmaxf(amx_, mx_);                                                                                   \
         }                                                                                                            \
         uint8_t* rw_ = sA + (BUF) * A_BYTES + p * RSA + (c & 1) * 8;                                                 \

@@ -28,13 +28,7 @@ __device__ __forceinline__ float act_fn(float v, int act) {
 __device__ __forceinline__ void put8(uint8_t* line, const float* v) {
   range_guard8(v);
   half8 hi, lo;
-#pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    _Float16 h_, l_;
-    split_f16(v[j], h_, l_);
-    hi[j] = h_;
-    lo[j] = l_;
-  }
+  split_vec(v, hi, lo);
   *reinterpret_cast<half8*>(line) = hi;
   *reinterpret_cast<half8*>(line + 64) = lo;
 }

@@ -24,13 +24,7 @@ __device__ __forceinline__ float act_fn(float v, int act) {
 __device__ __forceinline__ void put8(uint8_t* line, const float* v) {
   range_guard8(v);
   half8 hi, lo;
-#pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    _Float16 h_, l_;
-    split_f16(v[j], h_, l_);
-    hi[j] = h_;
-    lo[j] = l_;
-  }
+  split_vec(v, hi, lo);
   *reinterpret_cast<half8*>(line) = hi;
   *reinterpret_cast<half8*>(line + 64) = lo;
 }
@@ -179,13 +173,8 @@ __global__ __launch_bounds__(256) void flow_prep_tiled_kernel(const float* __res
     for (int c = 0; c < 4; ++c) {
       half8 hi, lo;
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        gm = fmaxf(gm, fabsf(v[8 * c + j]));
-        _Float16 h_, l_;
-        split_f16(v[8 * c + j], h_, l_);
-        hi[j] = h_;
-        lo[j] = l_;
-      }
+      for (int j = 0; j < 8; ++j) gm = fmaxf(gm, fabsf(v[8 * c + j]));
+      split_vec(v + 8 * c, hi, lo);
       *reinterpret_cast<half8*>(line + c * 16) = hi;
       *reinterpret_cast<half8*>(line + c * 16 + 64) = lo;
     }
