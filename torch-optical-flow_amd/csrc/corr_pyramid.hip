@@ -43,6 +43,7 @@ struct PyramidArgs {
   float scale;      // sqrt(C) as torch computes it (float sqrt of float(C))
   float inv_scale;  // exact 1/scale when scale is a power of two (multiply == divide bit-for-bit)
   int scale_pow2;
+  int stagger_cycles, stagger_mode;  // experiments only (oflow_exp_set_pyramid_stagger); 0 in the product
 };
 
 template <bool VEC>
@@ -406,6 +407,14 @@ __global__ __launch_bounds__(kThreads, 2) void corr_pyramid_s32_kernel(PyramidAr
   __shared__ __attribute__((aligned(16))) uint8_t sB[kBN * 128];
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  if (p.stagger_cycles > 0 && blockIdx.z == 0) {  // experiment: start some of the first wave of workgroups late
+    const unsigned id = blockIdx.x;
+    const bool late = p.stagger_mode == 1 ? (id >= 256u && id < 512u) : ((id & 1u) && id < 512u);
+    if (late) {
+      const unsigned long long t0 = __builtin_amdgcn_s_memtime();
+      while (__builtin_amdgcn_s_memtime() - t0 < static_cast<unsigned long long>(p.stagger_cycles)) __builtin_amdgcn_s_sleep(8);
+    }
+  }
   int tile, qblk;
   gemm_tile((p.N + kBM - 1) / kBM, p.tiles_x * ((p.H + kTR - 1) / kTR), tile, qblk);
   const int ty0 = (tile / p.tiles_x) * kTR;
@@ -530,6 +539,13 @@ __global__ __launch_bounds__(256) void avgpool2x2_tiled_kernel(const float* __re
 }  // namespace oflow
 
 using namespace oflow;
+
+static int g_pyr_stagger_cycles = 0, g_pyr_stagger_mode = 1;
+// experiment hook (not part of include/oflow.h): delay part of the split pyramid's first workgroups by `cycles`
+extern "C" void oflow_exp_set_pyramid_stagger(int cycles, int mode) {
+  g_pyr_stagger_cycles = cycles;
+  g_pyr_stagger_mode = mode;
+}
 
 extern "C" long long oflow_corr_tiled_level_floats(int H_l, int W_l) {
   if (H_l <= 0 || W_l <= 0) return 0;
@@ -659,6 +675,8 @@ extern "C" int oflow_corr_pyramid_tiled_s32(const void* d_fmap1_s32, const void*
   int e2 = 0;
   p.scale_pow2 = (frexpf(p.scale, &e2) == 0.5f) ? 1 : 0;
   p.inv_scale = p.scale_pow2 ? 1.0f / p.scale : 0.0f;
+  p.stagger_cycles = g_pyr_stagger_cycles;
+  p.stagger_mode = g_pyr_stagger_mode;
   const dim3 grid(p.tiles_x * ((H + kTR - 1) / kTR) * ((p.N + kBM - 1) / kBM), 1, B);
   hipLaunchKernelGGL((corr_pyramid_s32_kernel<true>), grid, dim3(kThreads), 0, s, p,
                      static_cast<const uint8_t*>(d_fmap1_s32), static_cast<const uint8_t*>(d_fmap2_s32));
