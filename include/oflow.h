@@ -225,6 +225,14 @@ int oflow_set_range_flag(unsigned int* d_flag);
  * range guard of RAFT.forward, methods/raft/model/raft.py:87-147, is this build's addition). */
 int oflow_range_flag_exchange(unsigned int* d_flag, unsigned int* d_out, void* stream);
 
+/* Instrumentation (bench.py's per-kernel timings; replaces nothing in the reference): HIP timing events that can be
+ * recorded inside a stream capture as external event-record nodes (external != 0), so every replay of the graph
+ * re-records them; oflow_timing_event_elapsed_ms = hipEventElapsedTime(end - start). Status OFLOW_OK or a HIP error. */
+int oflow_timing_event_create(void** ev);
+int oflow_timing_event_destroy(void* ev);
+int oflow_timing_event_record(void* ev, void* stream, int external);
+int oflow_timing_event_elapsed_ms(void* start, void* end, float* ms);
+
 int oflow_flow_head2_s32(const void* d_x, long long x_pixel_stride, int in_groups, const float* d_weight,
                          const float* d_bias, int B, int H, int W, float* d_coords, void* stream);
 /* oflow_corr_lookup_tiled_nhwc_f32: the tiled lookup as fp32 NHWC rows [B*H*W][row_floats] (d_out 16-B aligned) in the

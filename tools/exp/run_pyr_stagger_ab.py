@@ -17,7 +17,7 @@ import torch  # noqa: E402
 
 from optical_flow import _native as N  # noqa: E402
 
-ARMS = [(0, 1), (18000, 1), (37000, 1), (55000, 1), (37000, 2)]
+ARMS = [(0, 1), (18000, 1), (37000, 2)] + ([(0, 5)] if os.environ.get('EPI_ONLY') else [])
 
 
 def main():
@@ -35,6 +35,8 @@ def main():
         out = [t.clone() for t in N.corr_pyramid_tiled_s32(s1, s2, 4).levels]
         if ref is None:
             ref = out
+        elif arm[1] & 4:
+            pass  # the epilogue-only ablation stores zeros
         else:
             same = same and all(torch.equal(a, b) for a, b in zip(ref, out))
     del ref

@@ -25,6 +25,41 @@ extern "C" int oflow_range_flag_exchange(unsigned int* d_flag, unsigned int* d_o
   return oflow::launch_status();
 }
 
+// Instrumentation (bench.py's per-kernel timings; not a reference interface): HIP timing events that can also be
+// recorded inside a stream capture as external event-record nodes, so that every replay of the graph re-records them
+// (torch.cuda.Event refuses external records on ROCm). Status: OFLOW_OK or a HIP error code.
+extern "C" int oflow_timing_event_create(void** ev) {
+  if (!ev) return OFLOW_E_NULL;
+  hipEvent_t e = nullptr;
+  const hipError_t r = hipEventCreate(&e);
+  *ev = e;
+  return static_cast<int>(r);
+}
+extern "C" int oflow_timing_event_destroy(void* ev) { return static_cast<int>(hipEventDestroy(static_cast<hipEvent_t>(ev))); }
+extern "C" int oflow_timing_event_record(void* ev, void* stream, int external) {
+  hipEvent_t e = static_cast<hipEvent_t>(ev);
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  if (!external) return static_cast<int>(hipEventRecord(e, s));
+  // during a capture: an event-record node appended to the stream's capture dependencies (ROCm 7.2 rejects
+  // hipEventRecordWithFlags(hipEventRecordExternal) on a capturing stream with "invalid argument")
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  unsigned long long id = 0;
+  hipGraph_t g = nullptr;
+  const hipGraphNode_t* deps = nullptr;
+  size_t nd = 0;
+  hipError_t r = hipStreamGetCaptureInfo_v2(s, &cs, &id, &g, &deps, &nd);
+  if (r != hipSuccess) return static_cast<int>(r);
+  if (cs != hipStreamCaptureStatusActive) return static_cast<int>(hipEventRecord(e, s));
+  hipGraphNode_t node = nullptr;
+  r = hipGraphAddEventRecordNode(&node, g, deps, nd, e);
+  if (r != hipSuccess) return static_cast<int>(r);
+  return static_cast<int>(hipStreamUpdateCaptureDependencies(s, &node, 1, hipStreamSetCaptureDependencies));
+}
+extern "C" int oflow_timing_event_elapsed_ms(void* start, void* end, float* ms) {
+  if (!ms) return OFLOW_E_NULL;
+  return static_cast<int>(hipEventElapsedTime(ms, static_cast<hipEvent_t>(start), static_cast<hipEvent_t>(end)));
+}
+
 extern "C" const char* oflow_status_string(int status) {
   switch (status) {
     case OFLOW_OK: return "ok";

@@ -409,7 +409,7 @@ __global__ __launch_bounds__(kThreads, 2) void corr_pyramid_s32_kernel(PyramidAr
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   if (p.stagger_cycles > 0 && blockIdx.z == 0) {  // experiment: start some of the first wave of workgroups late
     const unsigned id = blockIdx.x;
-    const bool late = p.stagger_mode == 1 ? (id >= 256u && id < 512u) : ((id & 1u) && id < 512u);
+    const bool late = (p.stagger_mode & 3) == 1 ? (id >= 256u && id < 512u) : ((id & 1u) && id < 512u);
     if (late) {
       const unsigned long long t0 = __builtin_amdgcn_s_memtime();
       while (__builtin_amdgcn_s_memtime() - t0 < static_cast<unsigned long long>(p.stagger_cycles)) __builtin_amdgcn_s_sleep(8);
@@ -421,8 +421,8 @@ __global__ __launch_bounds__(kThreads, 2) void corr_pyramid_s32_kernel(PyramidAr
   const int tx0 = (tile % p.tiles_x) * kTC;
   const int i0 = qblk * kBM;
   const int b = blockIdx.z;
-  const int G = p.C >> 5;
-  const int ps = G * 128;  // bytes per pixel row
+  const int ps = (p.C >> 5) * 128;  // bytes per pixel row
+  const int G = (p.stagger_mode & 4) ? 0 : (p.C >> 5);  // experiment (mode bit 2): no main loop, epilogue alone
   const uint8_t* A0 = F1s + (size_t)b * p.N * ps;
   const uint8_t* B0 = F2s + (size_t)b * p.N * ps;
 

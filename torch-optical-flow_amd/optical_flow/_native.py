@@ -77,6 +77,10 @@ SYMBOLS = (
     "oflow_set_range_flag",
     "oflow_range_flag_exchange",
     "oflow_flow_head_col2im_f32",
+    "oflow_timing_event_create",
+    "oflow_timing_event_destroy",
+    "oflow_timing_event_record",
+    "oflow_timing_event_elapsed_ms",
 )
 
 _lib = None
@@ -101,9 +105,40 @@ def _count(exec_f16: int, useful: int, fma: int = 0) -> None:
 
 def set_event_recorder(recorder):
     """Record a HIP event pair on the launch stream around every kernel launch (bench instrumentation).
-    ``recorder`` is a dict (op name -> list of (start, end) ``torch.cuda.Event``) or None to stop."""
+    ``recorder`` is a dict (op name -> list of (start, end) events) or None to stop. The events are
+    ``torch.cuda.Event``s, or ``TimingEvent``s when the recorder holds ``"_native": True`` -- those may be recorded
+    inside a stream capture (external event-record nodes: each replay of the graph re-records them)."""
     global _recorder
     _recorder = recorder
+
+
+class TimingEvent:
+    """A HIP timing event of liboflow_hip.so (oflow_timing_event_*): ``record(stream)`` on a capturing stream records
+    it as an external event node of the graph (torch.cuda.Event refuses that on ROCm); ``elapsed_time(end)`` in ms,
+    as torch.cuda.Event's."""
+
+    __slots__ = ("ev",)
+
+    def __init__(self):
+        ev = ctypes.c_void_p()
+        _check(load().oflow_timing_event_create(ctypes.byref(ev)), "timing_event_create")
+        self.ev = ev
+
+    def record(self, stream: "torch.cuda.Stream") -> None:
+        ext = 1 if torch.cuda.is_current_stream_capturing() else 0
+        _check(load().oflow_timing_event_record(self.ev, ctypes.c_void_p(stream.cuda_stream), ext), "timing_event_record")
+
+    def elapsed_time(self, end: "TimingEvent") -> float:
+        ms = ctypes.c_float()
+        _check(load().oflow_timing_event_elapsed_ms(self.ev, end.ev, ctypes.byref(ms)), "timing_event_elapsed_ms")
+        return float(ms.value)
+
+    def __del__(self):
+        try:
+            if _lib is not None and self.ev:
+                _lib.oflow_timing_event_destroy(self.ev)
+        except Exception:  # noqa: BLE001 (interpreter shutdown)
+            pass
 
 
 # ops whose launches are bracketed by events when a recorder is set (others only if the recorder has "*": True)
@@ -121,13 +156,13 @@ class _Timed:
 
     def __enter__(self):
         if self.stream is not None:
-            self.ev0 = torch.cuda.Event(enable_timing=True)
+            self.ev0 = TimingEvent() if _recorder.get("_native") else torch.cuda.Event(enable_timing=True)
             self.ev0.record(self.stream)
         return self
 
     def __exit__(self, *exc):
         if self.stream is not None and exc[0] is None and _recorder is not None:
-            ev1 = torch.cuda.Event(enable_timing=True)
+            ev1 = TimingEvent() if _recorder.get("_native") else torch.cuda.Event(enable_timing=True)
             ev1.record(self.stream)
             _recorder.setdefault(self.what, []).append((self.ev0, ev1))  # type: ignore[union-attr]
         return False
@@ -233,6 +268,14 @@ def load() -> ctypes.CDLL:
     lib.oflow_set_range_flag.argtypes = [P]
     lib.oflow_range_flag_exchange.restype = I
     lib.oflow_range_flag_exchange.argtypes = [P, P, P]
+    lib.oflow_timing_event_create.restype = I
+    lib.oflow_timing_event_create.argtypes = [ctypes.POINTER(ctypes.c_void_p)]
+    lib.oflow_timing_event_destroy.restype = I
+    lib.oflow_timing_event_destroy.argtypes = [P]
+    lib.oflow_timing_event_record.restype = I
+    lib.oflow_timing_event_record.argtypes = [P, P, I]
+    lib.oflow_timing_event_elapsed_ms.restype = I
+    lib.oflow_timing_event_elapsed_ms.argtypes = [P, P, ctypes.POINTER(ctypes.c_float)]
     lib.oflow_flow_head_col2im_f32.restype = I
     lib.oflow_flow_head_col2im_f32.argtypes = [P, P, I, I, I, P, P]
     v = lib.oflow_abi_version()
