@@ -19,6 +19,12 @@ launch / mean launch time from HIP events recorded on the launch stream inside t
 the corr pyramid kernel's MFMA rate, ``epe_vs_reference`` (the LAST TIMED STEP's flows for the golden batch's pairs
 against the reference's own flows for them), and the oracle (PyTorch-CPU restatement) timed on this host's cores on
 the workload's per-GPU batch. ``--pairs-per-gpu 1 --iters 24`` is predict.py's batch-1 latency case.
+
+r05: the RAFT workloads 'sintel' and 'kitti' replay each rank's forward from a HIP graph by default (model/graph.py:
+the same kernels, both pair lanes, captured once before the timed region; inputs copied in per step): the same work
+per step without the host's per-launch Python. The per-kernel timings then come from event-record nodes captured into
+the graph around the timed launches (liboflow's native timing events; torch's refuse that on ROCm), read after the
+timed region: they time its last replay. ``--eager`` times the eager forward instead.
 """
 from __future__ import annotations
 
@@ -359,7 +365,9 @@ def main() -> int:
     ap.add_argument("--conv-events", action="store_true", help="also time every update-block conv launch")
     ap.add_argument("--update-impl", default="split", choices=["split", "fused", "module"])
     ap.add_argument("--graph", action="store_true",
-                    help="replay each rank's forward from a HIP graph (model/graph.py: one launch per step)")
+                    help="replay each rank's forward from a HIP graph (model/graph.py: one launch per step); the default "
+                         "for 'sintel' / 'kitti' with --inflight 1")
+    ap.add_argument("--eager", action="store_true", help="run the eager forward (no HIP graph)")
     ap.add_argument("--no-conv-benchmark", action="store_true",
                     help="disable torch.backends.cudnn.benchmark (MIOpen exhaustive find of the conv algorithms)")
     ap.add_argument("--inflight", type=int, default=1,
@@ -374,6 +382,13 @@ def main() -> int:
     ap.add_argument("--range-guard", default=None, choices=["sync", "deferred", "off"],
                     help="RAFT.range_guard (default: the model's, 'deferred': checked after the timed region)")
     args = ap.parse_args()
+    if args.graph and args.eager:
+        print("bench: --graph and --eager exclude each other", file=sys.stderr)
+        return 2
+    # graph replay by default for the RAFT workloads (one capture per rank; a second step in flight would share its
+    # static buffers, so --inflight > 1 stays eager)
+    args.graph = args.graph or (not args.eager and args.workload in ("sintel", "kitti") and args.inflight == 1
+                                and args.update_impl == "split")
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -441,17 +456,25 @@ def main() -> int:
         return low, padder.unpad(up)
 
     fwd = forward
+    graph_rec = None
     if args.graph and args.workload != "corr":
         from model.graph import GraphedRAFT
 
         # capture this rank's shard shape (padded), then every step copies the shard in and replays
         pp = padder.pad(*(torch.zeros((ppg, 3, h, w), device=dev),) * 2)
+        # per-kernel timing inside the graph: native event-record nodes captured around the timed launches, re-recorded
+        # by every replay (read after the timed region: they time its last replay)
+        graph_rec = None if args.no_events else ({"_native": True, "*": True} if args.conv_events else {"_native": True})
         with torch.inference_mode():
-            graphed = GraphedRAFT(model, pp[0], pp[1], iters=iters)
+            graphed = GraphedRAFT(model, pp[0], pp[1], iters=iters, recorder=graph_rec)
 
         def fwd(s0, s1):
             p0, p1 = padder.pad(s0, s1)
             low, up = graphed(p0, p1)
+            if world > 1:
+                # the graph's outputs are overwritten by the next replay, while this step's gathers may still be
+                # reading them on the communicator's stream (pipelined driver): hand them copies
+                return low.clone(), padder.unpad(up).clone()
             return low, padder.unpad(up)
 
     def step():
@@ -483,7 +506,7 @@ def main() -> int:
     with torch.inference_mode():
         run_steps(max(args.warmup, 1 if pipelined else len(streams)))
         torch.cuda.synchronize(dev)
-        # graph replays launch no Python, so no per-kernel events (the roofline comes from an eager run)
+        # graph replays launch no Python: their per-kernel events are the graph's own nodes (graph_rec, captured above)
         rec = ({"*": True} if args.conv_events else {}) if not (args.no_events or args.graph) else None
         _native.set_event_recorder(rec)
         if world > 1:
@@ -496,16 +519,19 @@ def main() -> int:
             dist.barrier()
         elapsed = time.perf_counter() - t0
         _native.set_event_recorder(None)
+        rec_forwards = args.steps  # forwards the recorder's events cover
+        if args.graph and graph_rec is not None:
+            rec, rec_forwards = graph_rec, 1  # the last replay's launches
         if getattr(model, "range_guard", "off") == "deferred":
             model.check_range(dev)  # every timed forward's split operands were in range (raises otherwise)
         if rank == 0 and gtag:
             epe = step_epe(out, gtag, gfix, global_batch)
         # one more (untimed) forward with the per-launch flop counter: the step roofline
         step_flops = None
-        if args.workload != "corr" and not args.graph and not args.no_step_flops:
+        if args.workload != "corr" and not args.no_step_flops:
             cnt = {}
             _native.set_flop_counter(cnt)
-            fwd(img0[:ppg] if img0 is not None else torch.zeros((ppg, 3, h, w), device=dev),
+            forward(img0[:ppg] if img0 is not None else torch.zeros((ppg, 3, h, w), device=dev),
                 img1[:ppg] if img1 is not None else torch.zeros((ppg, 3, h, w), device=dev))
             _native.set_flop_counter(None)
             torch.cuda.synchronize(dev)
@@ -566,7 +592,7 @@ def main() -> int:
     }
     if rec and args.conv_events:
         convs = {k: v for k, v in rec.items() if k.startswith("conv") or k == "flow_prep"}
-        line["conv_ms_per_step"] = {k: round(sum(a.elapsed_time(b) for a, b in v) / args.steps, 3) for k, v in convs.items()}
+        line["conv_ms_per_step"] = {k: round(sum(a.elapsed_time(b) for a, b in v) / rec_forwards, 3) for k, v in convs.items()}
     if rec and alt:
         lk = rec.get("corr_lookup_otf", [])
         pp = rec.get("corr_otf_prepare", [])
@@ -579,7 +605,7 @@ def main() -> int:
         lk = rec["corr_lookup_convc1"]
         pk = rec.get("corr_pyramid", [])
         lk_ms = mean_ms(lk)
-        lanes = max(1, len(lk) // (iters * args.steps))
+        lanes = max(1, len(lk) // (iters * rec_forwards))
         lk_bytes = fused_lookup_bytes(ppg, dims, lanes) // lanes
         flops = fused_lookup_flops(ppg, dims) // lanes
         ach = lk_bytes / (lk_ms * 1e-3) / 1e9

@@ -17,6 +17,8 @@ from typing import Tuple
 import torch
 from torch import Tensor
 
+from optical_flow import _native
+
 from . import update as _update
 
 # A multi-pair forward is captured with its pair lanes (RAFT.pair_lanes) but without the per-lane side streams of the
@@ -35,12 +37,18 @@ class GraphedRAFT:
         image0, image1: (B, 3, H, W) example inputs (H, W divisible by 8: pad with ``InputPadder`` first)
         iters: GRU iterations
         warmup: eager forwards on a side stream before capture (allocator and weight caches settle)
+        recorder: optional per-kernel timing recorder (``_native.set_event_recorder``; must hold ``"_native": True``),
+            active during the capture only: its event pairs become event-record nodes of the graph, re-recorded by
+            every replay, so after a replay they time that replay's launches (bench.py --graph)
 
     Calling the object with new images of the same shape returns ``(flow_low, flow_up)``: tensors owned by the graph,
     overwritten by the next call (clone them to keep them).
     """
 
-    def __init__(self, model, image0: Tensor, image1: Tensor, iters: int = 12, warmup: int = 2) -> None:
+    def __init__(self, model, image0: Tensor, image1: Tensor, iters: int = 12, warmup: int = 2, recorder=None) -> None:
+        if recorder is not None and not recorder.get("_native"):
+            raise ValueError("GraphedRAFT: a recorder needs native timing events ({'_native': True})")
+        self.recorder = recorder
         if not image0.is_cuda:
             raise RuntimeError("GraphedRAFT: the inputs must be ROCm GPU tensors")
         self.model, self.iters = model, iters
@@ -71,11 +79,16 @@ class GraphedRAFT:
             # capture_active(): the pair lanes' streams join the capture through event waits and on ROCm do not report
             # themselves as capturing; the weight caches must not wait on their (pre-capture) events from any of them
             _update._CAPTURE_DEPTH[0] += 1
+            prev = _native._recorder
+            if self.recorder is not None:
+                _native.set_event_recorder(self.recorder)
             try:
                 with torch.cuda.graph(self.graph, stream=side):
                     self.flow_low, self.flow_up = model(self.image0, self.image1, iters=iters, test_mode=True)
             finally:
                 _update._CAPTURE_DEPTH[0] -= 1
+                if self.recorder is not None:
+                    _native.set_event_recorder(prev)
 
     def __call__(self, image0: Tensor, image1: Tensor) -> Tuple[Tensor, Tensor]:
         if image0.shape != self.image0.shape or image1.shape != self.image1.shape:

@@ -125,8 +125,9 @@ class TimingEvent:
         self.ev = ev
 
     def record(self, stream: "torch.cuda.Stream") -> None:
-        ext = 1 if torch.cuda.is_current_stream_capturing() else 0
-        _check(load().oflow_timing_event_record(self.ev, ctypes.c_void_p(stream.cuda_stream), ext), "timing_event_record")
+        # external = 1: the library asks HIP whether `stream` is capturing (a pair lane forked inside a capture is,
+        # though torch.cuda.is_current_stream_capturing() does not say so on ROCm) and records a plain event if not
+        _check(load().oflow_timing_event_record(self.ev, ctypes.c_void_p(stream.cuda_stream), 1), "timing_event_record")
 
     def elapsed_time(self, end: "TimingEvent") -> float:
         ms = ctypes.c_float()
