@@ -368,6 +368,7 @@ def main() -> int:
                     help="replay each rank's forward from a HIP graph (model/graph.py: one launch per step); the default "
                          "for 'sintel' / 'kitti' with --inflight 1")
     ap.add_argument("--eager", action="store_true", help="run the eager forward (no HIP graph)")
+    ap.add_argument("--lanes", type=int, default=None, help="RAFT.pair_lanes (default: the model's)")
     ap.add_argument("--no-conv-benchmark", action="store_true",
                     help="disable torch.backends.cudnn.benchmark (MIOpen exhaustive find of the conv algorithms)")
     ap.add_argument("--inflight", type=int, default=1,
@@ -417,6 +418,8 @@ def main() -> int:
     model.update_impl = args.update_impl
     if args.range_guard:
         model.range_guard = args.range_guard
+    if args.lanes:
+        model.pair_lanes = args.lanes
 
     img0 = img1 = None
     if args.workload == "corr":  # configs[1]: fmaps (B, 256, 128, 128) ~ N(0, 1.45^2), coords = grid + N(0, 4^2)

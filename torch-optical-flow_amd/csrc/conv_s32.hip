@@ -55,6 +55,13 @@ __device__ __forceinline__ int swz(int row) { return (row >> 1) & 7; }
 #ifndef OFLOW_PAD_ROWS
 #define OFLOW_PAD_ROWS 1
 #endif
+// register-direct weights: the halo double-buffered in LDS (1): group g+1's halo is written into the buffer group g-1
+// used while group g's MFMAs run, one barrier per group instead of two around a single buffer's swap. Bit-identical,
+// but the step is 0.1-0.3 ms slower (the doubled halo, up to 74 KB per workgroup, crowds the other lane's workgroups
+// off the CUs: profiles/r05/s25_step_ab.log), so the single buffer (0) stays the default.
+#ifndef OFLOW_HALO_DB
+#define OFLOW_HALO_DB 0
+#endif
 
 constexpr int kTY = 4, kTX = 32;  // default tile: kTY rows x kTX columns
 
@@ -219,7 +226,8 @@ __global__ __launch_bounds__(64 * WM * WN, WM * WN == 8 ? 1 : 2) void conv_s32_k
   constexpr int A_BYTES = NPIX * RSA, B_BYTES = BN * RSB;
   static_assert(!BREG || (T > 1 && (WM == 1 || WM == 2 || WM == 4) && BN == 32 * WN && AIN == kInS32),
                 "register-direct B: T > 1, WM x WN waves of one 32-channel tile each");
-  constexpr int MAIN_BYTES = (ADB ? 2 : 1) * A_BYTES + (BREG ? 0 : 2 * B_BYTES);
+  constexpr bool HDB = BREG && OFLOW_HALO_DB;  // double-buffered halo (register-direct kernels)
+  constexpr int MAIN_BYTES = ((ADB || HDB) ? 2 : 1) * A_BYTES + (BREG ? 0 : 2 * B_BYTES);
   constexpr int TS = BN + 4;              // epilogue tile row stride (floats)
   constexpr int EPI_BYTES = BM * TS * 4;
   constexpr int LDS_BYTES = MAIN_BYTES > EPI_BYTES ? MAIN_BYTES : EPI_BYTES;
@@ -506,9 +514,10 @@ __global__ __launch_bounds__(64 * WM * WN, WM * WN == 8 ? 1 : 2) void conv_s32_k
     const int ii_ = (I);                                                                                              \
     const int t_ = ii_ % T, ky_ = t_ / KW, kx_ = t_ - ky_ * KW;                                                       \
     const int chi_ = 2 * (S_) + hh, clo_ = 4 + 2 * (S_) + hh;                                                        \
+    const uint8_t* sAb_ = sA + (HDB && ((ii_ / T) & 1) ? A_BYTES : 0); /* group (I / T)'s halo buffer */          \
     _Pragma("unroll") for (int mt_ = 0; mt_ < MT; ++mt_) {                                                           \
       const int p_ = (wm * MT + mt_ + ky_) * HX + r + kx_;                                                           \
-      const uint8_t* row_ = sA + p_ * RSA;                                                                           \
+      const uint8_t* row_ = sAb_ + p_ * RSA;                                                                         \
       AH[mt_] = *reinterpret_cast<const half8*>(row_ + (chi_ << 4));                                                 \
       AL[mt_] = *reinterpret_cast<const half8*>(row_ + (clo_ << 4));                                                 \
     }                                                                                                                \
@@ -535,8 +544,8 @@ __global__ __launch_bounds__(64 * WM * WN, WM * WN == 8 ? 1 : 2) void conv_s32_k
   if constexpr (VSLIDE) {
     constexpr int NR = MT + KH - 1;  // halo rows per group
     half8 V[NR][2][2];               // [halo row][sub-step][hi, lo]
-    auto rd = [&](int hr, int sub) {
-      const uint8_t* row_ = sA + (hr * HX + r) * RSA;
+    auto rd = [&](int hr, int sub, int grp) {
+      const uint8_t* row_ = sA + (HDB && (grp & 1) ? A_BYTES : 0) + (hr * HX + r) * RSA;
       V[hr][sub][0] = *reinterpret_cast<const half8*>(row_ + ((2 * sub + hh) << 4));
       V[hr][sub][1] = *reinterpret_cast<const half8*>(row_ + ((4 + 2 * sub + hh) << 4));
     };
@@ -551,7 +560,7 @@ __global__ __launch_bounds__(64 * WM * WN, WM * WN == 8 ? 1 : 2) void conv_s32_k
       }
     };
 #pragma unroll
-    for (int m = 0; m < MT; ++m) rd(m, 0);
+    for (int m = 0; m < MT; ++m) rd(m, 0, 0);
     for (int g0 = 0; g0 < a.kg; g0 += GPB) {
 #pragma unroll
       for (int j = 0; j < GPB * T; ++j) {
@@ -561,21 +570,26 @@ __global__ __launch_bounds__(64 * WM * WN, WM * WN == 8 ? 1 : 2) void conv_s32_k
         u32x4 (&bc)[4] = bq[j % RING];
         if (t == 0) {
 #pragma unroll
-          for (int m = 0; m < MT; ++m) rd(m, 1);
+          for (int m = 0; m < MT; ++m) rd(m, 1, gg);
         } else {
-          rd(t + MT - 1, 1);
+          rd(t + MT - 1, 1, gg);
         }
         mf(t, 0, bc);
         if (t == T - 1) {
-          __syncthreads();
-          OFLOW_WRITE_A(ra, 0, gg + 1 < a.kg ? gg + 1 : gg);
+          if constexpr (HDB) {
+            // group gg+1's halo into the other buffer (last read in group gg-1, before the previous barrier)
+            OFLOW_WRITE_A(ra, (gg + 1) & 1, gg + 1 < a.kg ? gg + 1 : gg);
+          } else {
+            __syncthreads();
+            OFLOW_WRITE_A(ra, 0, gg + 1 < a.kg ? gg + 1 : gg);
+          }
           const int g2 = gg + 2 < a.kg ? gg + 2 : a.kg - 1;
           OFLOW_LOAD_A(ra, g2);
           __syncthreads();
 #pragma unroll
-          for (int m = 0; m < MT; ++m) rd(m, 0);  // the next group's first tap (rows 0 .. MT-1: free since tap MT-1)
+          for (int m = 0; m < MT; ++m) rd(m, 0, gg + 1);  // the next group's first tap (rows 0 .. MT-1: free since tap MT-1)
         } else {
-          rd(t + MT, 0);  // the next tap's new row
+          rd(t + MT, 0, gg);  // the next tap's new row
         }
         mf(t, 1, bc);
         load_b(bc, i_ + RING < S ? i_ + RING : S - 1);
@@ -594,8 +608,12 @@ __global__ __launch_bounds__(64 * WM * WN, WM * WN == 8 ? 1 : 2) void conv_s32_k
       OFLOW_READ_A(yah, yal, i_, 1);
       OFLOW_MFMAS_R(xah, xal, bc, 0);
       if (t == T - 1) {  // the halo swap: every wave done reading A(g); A(g+1) visible before its first read
-        __syncthreads();
-        OFLOW_WRITE_A(ra, 0, gg + 1 < a.kg ? gg + 1 : gg);
+        if constexpr (HDB) {
+          OFLOW_WRITE_A(ra, (gg + 1) & 1, gg + 1 < a.kg ? gg + 1 : gg);  // the other buffer (read last in group g-1)
+        } else {
+          __syncthreads();
+          OFLOW_WRITE_A(ra, 0, gg + 1 < a.kg ? gg + 1 : gg);
+        }
         const int g2 = gg + 2 < a.kg ? gg + 2 : a.kg - 1;
         OFLOW_LOAD_A(ra, g2);
         __syncthreads();
