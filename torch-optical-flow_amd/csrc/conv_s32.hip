@@ -959,9 +959,14 @@ __global__ __launch_bounds__(64 * WM * WN, WM * WN == 8 ? 1 : 2) void conv_s32_k
     } else if constexpr (EPI == 1) {
       // [z | r] gates (update.py:91-96): z = sigmoid -> a.z; r*h = sigmoid(r) * h -> S32 y0 (channel n - gch)
       if (n < a.gch) {
-        float* zp = a.z + P * a.gch + n;
+        // two 16-B stores per item (a.z rows of gch = 128 floats, n % 8 == 0: 32-B aligned); as 8 dword stores the
+        // compiler could not prove the alignment and each wave instruction wrote 64 lanes' 4 B, 32 B apart
+        float4* zp = reinterpret_cast<float4*>(a.z + P * a.gch + n);
+        float zv[8];
 #pragma unroll
-        for (int j = 0; j < 8; ++j) zp[j] = hwx ? sigmoid_hw(v[j]) : 1.0f / (1.0f + expf(-v[j]));
+        for (int j = 0; j < 8; ++j) zv[j] = hwx ? sigmoid_hw(v[j]) : 1.0f / (1.0f + expf(-v[j]));
+        zp[0] = make_float4(zv[0], zv[1], zv[2], zv[3]);
+        zp[1] = make_float4(zv[4], zv[5], zv[6], zv[7]);
       } else {
         float rh[8];
 #pragma unroll
