@@ -10,7 +10,7 @@ i=0
 for ctr in TCC_EA0_RDREQ_sum WRITE_SIZE; do
   i=$((i+1))
   timeout -s KILL 120 rocprofv3 --pmc $ctr --kernel-include-regex "corr_convc1|corr_lookup_tiled|warp_strip" --output-format csv \
-    -d gpurun_out/pmc/p$i -o run -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline > gpurun_out/pmc/p$i.log 2>&1
+    -d gpurun_out/pmc/p$i -o run -- python3 bench.py --eager --steps 3 --warmup 1 --no-cpu-baseline > gpurun_out/pmc/p$i.log 2>&1
   rc=$?
   echo "pass $i ($ctr) rc=$rc"
   [ $rc -eq 0 ] || exit $rc

@@ -15,7 +15,7 @@ for ctrs in \
   "SQ_INSTS_VALU SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_SALU SQ_INSTS_VMEM SQ_ACTIVE_INST_LDS SQ_INSTS_MFMA GRBM_GUI_ACTIVE"; do
   i=$((i+1))
   timeout -s KILL 150 rocprofv3 --pmc $ctrs --kernel-include-regex "$KRE" --output-format csv \
-    -d gpurun_out/pmcm/p$i -o run -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline > gpurun_out/pmcm/p$i.log 2>&1
+    -d gpurun_out/pmcm/p$i -o run -- python3 bench.py --eager --steps 2 --warmup 1 --no-cpu-baseline > gpurun_out/pmcm/p$i.log 2>&1
   rc=$?
   echo "pass $i rc=$rc"
   [ $rc -eq 0 ] || exit $rc
