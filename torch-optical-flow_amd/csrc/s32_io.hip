@@ -151,35 +151,38 @@ __global__ __launch_bounds__(256) void flow_prep_tiled_kernel(const float* __res
     sF[e] = f;
   }
   __syncthreads();
+  // r05: the tile's output (128 pixels x 4 groups = 512 lines of 128 B, pixel-major, contiguous within a tile row) as
+  // 16-B chunks with consecutive lanes on consecutive chunks: a wave store instruction writes 8 whole lines (1 KB
+  // contiguous) instead of 64 scattered 16-B pieces of 64 lines. Chunk c of line (pixel, group g): c < 4 the hi halves
+  // of the group's values 8c .. 8c+7 (taps 16g + 4c .. +3, x and y), c >= 4 the lo halves of values 8(c-4) ..
+  float gm = 0.f;
+#pragma unroll 4
+  for (int i = 0; i < (kFpTH * kFpTW * G * 8) / 256; ++i) {
+    const int k = threadIdx.x + 256 * i, line = k >> 3, c = k & 7;
+    const int pl = line >> 2, g = line & 3, py = pl / kFpTW, px = pl - py * kFpTW;
+    const int y = ty0 + py, x = tx0 + px;
+    if (y >= H || x >= W) continue;
+    float v[8];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int tt = g * 16 + (c & 3) * 4 + e;
+      float2 f = make_float2(0.f, 0.f);
+      if (tt < KS * KS) f = sF[(py + tt / KS) * kFpWW + px + tt % KS];
+      v[2 * e] = f.x;
+      v[2 * e + 1] = f.y;
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) gm = fmaxf(gm, fabsf(v[j]));
+    half8 hi, lo;
+    split_vec(v, hi, lo);
+    const long long p = (long long)b * HW + (long long)y * W + x;
+    *reinterpret_cast<half8*>(pm + (p * G + g) * 128 + (c & 3) * 16 + (c >> 2) * 64) = (c >> 2) ? lo : hi;
+  }
+  range_guard(gm);  // (the centre tap is among the patch values: the flow channels below are covered)
   const int pl = threadIdx.x & (kFpTH * kFpTW - 1), py = pl / kFpTW, px = pl - py * kFpTW;
   const int y = ty0 + py, x = tx0 + px;
   if (y >= H || x >= W) return;
   const long long p = (long long)b * HW + (long long)y * W + x;
-  float gm = 0.f;
-#pragma unroll
-  for (int gi = 0; gi < 2; ++gi) {
-    const int g = 2 * gi + (threadIdx.x >> 7);  // threads 0-127: groups 0, 2; 128-255: groups 1, 3
-    float v[32];
-#pragma unroll
-    for (int k = 0; k < 16; ++k) {
-      const int tt = g * 16 + k;
-      float2 f = make_float2(0.f, 0.f);
-      if (tt < KS * KS) f = sF[(py + tt / KS) * kFpWW + px + tt % KS];
-      v[2 * k] = f.x;
-      v[2 * k + 1] = f.y;
-    }
-    uint8_t* line = pm + (p * G + g) * 128;
-#pragma unroll
-    for (int c = 0; c < 4; ++c) {
-      half8 hi, lo;
-#pragma unroll
-      for (int j = 0; j < 8; ++j) gm = fmaxf(gm, fabsf(v[8 * c + j]));
-      split_vec(v + 8 * c, hi, lo);
-      *reinterpret_cast<half8*>(line + c * 16) = hi;
-      *reinterpret_cast<half8*>(line + c * 16 + 64) = lo;
-    }
-  }
-  range_guard(gm);  // (the centre tap is among the patch values: the flow channels below are covered)
   if (threadIdx.x < 128 && d0) {
     const float2 f = sF[(py + R) * kFpWW + px + R];
     _Float16 hx, lx, hy, ly;
