@@ -365,6 +365,36 @@ def test_graphed_multi_pair_forward_equals_eager_two_lanes():
         assert torch.equal(lo_g, lo_e) and torch.equal(up_g, up_e)
 
 
+def test_graphed_forward_timing_event_nodes():
+    """bench.py's graph mode: a recorder with native timing events ({'_native': True}) given to GraphedRAFT is active
+    during the capture only; its event pairs around the fused lookup + convc1 and pyramid launches become event-record
+    nodes of the graph, re-recorded by every replay: after a replay each pair reads a positive duration (the launch's),
+    one pair per lane and iteration, and the flows still equal the eager forward's."""
+    from model.graph import GraphedRAFT
+    from optical_flow import _native
+
+    model = _model(RAFT)
+    a0, a1 = synthetic.synthetic_pair(3, 436, 1024, seed=33)
+    padder = InputPadder(a0.shape)
+    p0, p1 = (x.to(DEV) for x in padder.pad(a0, a1))
+    rec = {"_native": True}
+    with torch.inference_mode():
+        g = GraphedRAFT(model, p0, p1, iters=4, recorder=rec)
+        assert _native._recorder is None  # restored after the capture
+        lo_g, up_g = g(p0, p1)
+        torch.cuda.synchronize()
+        lk = rec["corr_lookup_convc1"]
+        assert len(lk) == 4 * 2  # iterations x pair lanes
+        first = [a.elapsed_time(b) for a, b in lk]
+        assert all(0.0 < t < 50.0 for t in first), first
+        assert len(rec["corr_pyramid"]) == 1 and rec["corr_pyramid"][0][0].elapsed_time(rec["corr_pyramid"][0][1]) > 0
+        g(p0, p1)  # a second replay re-records the same events
+        torch.cuda.synchronize()
+        assert all(0.0 < a.elapsed_time(b) < 50.0 for a, b in lk)
+        lo_e, up_e = model(p0, p1, iters=4, test_mode=True)
+    assert torch.equal(lo_g, lo_e) and torch.equal(up_g, up_e)
+
+
 @pytest.mark.parametrize("where", ["images", "convc1", "convc2"])
 def test_range_guard_raises_on_split_overflow(where):
     """The split-fp16 range guard (oflow_set_range_flag): an activation whose fp16 hi half overflows (|x| >= 65520) sets
