@@ -56,6 +56,7 @@ extern "C" {
 #define OFLOW_IN_F32_NORM 1
 #define OFLOW_IN_F32 2
 #define OFLOW_IN_IMG7S2 3
+#define OFLOW_IN_FLOW7 4
 
 int oflow_abi_version(void);
 const char* oflow_status_string(int status);
@@ -281,6 +282,12 @@ int oflow_corr_lookup_convc1_s32(const float* const* d_levels, const int* level_
  *   stages its 13 x 69 x 3 input window in LDS and builds the patch-matrix operand (channel t*3 + c, t = ky*7 + kx,
  *   in_groups 5 = 160 channels, weights packed with patches=True as for oflow_stem_patches_s32's matrix) from it, so
  *   no patch matrix is written (1x1 geometry, epilogue 0, block_n 64).
+ *   OFLOW_IN_FLOW7: the motion encoder's convf1 (update.py:116, a 7x7 / stride 1 / pad 3 conv of the 2-channel flow)
+ *   straight from coords1 d_x (B, 2, H, W) fp32 (x_pixel_stride ignored): flow = coords1 - the pixel grid (raft.py:129,
+ *   the fp32 subtraction of oflow_flow_prep_s32), each 4 x 32 output tile stages its 10 x 38 x 2 flow window in LDS
+ *   and builds the patch operand (channel t*2 + c, t = ky*7 + kx, in_groups 4 = 128 channels, weights packed with
+ *   patches=True as for oflow_flow_prep_s32's matrix) from it: bit for bit the conv of that matrix, which is then not
+ *   written (1x1 geometry, epilogue 0, block_n 128).
  * oflow_stem_patches_s32: 7x7/2 pad-3 patch matrix of a (B, C, H, W) fp32 image: S32 (B, ceil(H/2), ceil(W/2),
  *   out_groups) with channel t*C + c (t = ky*7 + kx), zeros past 49*C.
  * oflow_norm_stats_finalize: merge the partials (fp64 sums) -> alpha = 1/sqrt(var + eps), beta = -mean * alpha, [B][C].

@@ -245,6 +245,34 @@ def test_pack_s32_and_flow_prep():
         assert float((N.s32_to_f32(t)[:, 382:] - flow).abs().max()) <= 1e-6 * float(flow.abs().max())
 
 
+@pytest.mark.parametrize("b,h,w", [(4, 55, 128), (2, 11, 29), (1, 47, 156), (3, 5, 3)])
+def test_convf1_from_flow_equals_patch_matrix(b, h, w):
+    """convf1 straight from coords1 (N.FlowIn, OFLOW_IN_FLOW7: the flow window staged per tile, the patch operand built
+    in LDS) against the conv of flow_prep's patch matrix: bit-identical S32 outputs (same patch values, same k order),
+    ragged tiles and images smaller than a tile included; flow_prep without the matrix still writes the GRU inputs'
+    flow channels bit for bit."""
+    g = torch.Generator().manual_seed(h * 1000 + w)
+    coords = coords_grid(b, h, w, device=DEV) + (torch.randn(b, 2, h, w, generator=g) * 9).to(DEV)
+    conv = torch.nn.Conv2d(2, 128, 7, padding=3)
+    with torch.no_grad():
+        conv.weight.normal_(0.0, 0.05, generator=g)
+        conv.bias.normal_(0.0, 0.1, generator=g)
+    cw = N.ConvWeights(conv.weight.to(DEV), conv.bias.to(DEV), 128, patches=True)
+    pm = N.s32_empty(b, h, w, 4, DEV, zero=True)
+    hx = [N.s32_empty(b, h, w, 12, DEV, zero=True) for _ in range(2)]
+    N.flow_prep(coords, pm, (N.S32Slice(hx[0]), 382))
+    N.flow_prep(coords, None, (N.S32Slice(hx[1]), 382))
+    ys = [N.s32_empty(b, h, w, 4, DEV, zero=True) for _ in range(2)]
+    N.conv_s32(N.S32Slice(pm), cw, 128, "relu", y0=N.S32Slice(ys[0]))
+    N.conv_s32(N.FlowIn(coords), cw, 128, "relu", y0=N.S32Slice(ys[1]))
+    torch.cuda.synchronize()
+    assert torch.equal(ys[0], ys[1])
+    assert torch.equal(hx[0], hx[1])
+    ref = F.relu(F.conv2d(coords.double() - coords_grid(b, h, w, device=DEV).double(), conv.weight.to(DEV).double(),
+                          conv.bias.to(DEV).double(), padding=3))
+    assert float((N.s32_to_f32(ys[1]).double() - ref).abs().max()) <= 1e-4 * max(1.0, float(ref.abs().max()))
+
+
 @pytest.mark.parametrize("c,dst", [(100, 8), (37, 0), (256, 0), (8, 24)])
 def test_pack_s32_ragged_channels(c, dst):
     """pack_s32 with channel counts that end mid-group / mid-octet and destinations that start mid-group: every

@@ -122,7 +122,8 @@ struct ConvArgs {
   int exp_flags;           // experiments only (oflow_exp_set_conv_flags): bit 0 = the stem's element-wise window loop
 };
 // input formats of oflow_conv_s32_ex2
-constexpr int kInS32 = OFLOW_IN_S32, kInF32Norm = OFLOW_IN_F32_NORM, kInF32 = OFLOW_IN_F32, kInImg = OFLOW_IN_IMG7S2;
+constexpr int kInS32 = OFLOW_IN_S32, kInF32Norm = OFLOW_IN_F32_NORM, kInF32 = OFLOW_IN_F32, kInImg = OFLOW_IN_IMG7S2,
+              kInFlow = OFLOW_IN_FLOW7;
 // kInImg: the stem's 7x7/2 pad-3 window of a 3-channel image, staged per tile (TY = 4 rows x 32 columns)
 constexpr int kImgC = 3, kImgK = 7, kImgRows = (kTY - 1) * 2 + kImgK, kImgCols = (kTX - 1) * 2 + kImgK;
 // the window in LDS: [c][row][column parity][column / 2] (row pitch kImgPitch floats): output column x reads window
@@ -214,7 +215,16 @@ __global__ __launch_bounds__(64 * WM * WN, WM * WN == 8 ? 1 : 2) void conv_s32_k
   // The stem (kInImg) builds A from the image window already in LDS, so nothing is gained by building A(i+1) beside
   // A(i): one A buffer and the halo-swap schedule (a barrier before each rebuild) -- 50.5 instead of 68.9 KB of LDS,
   // three workgroups per CU instead of two (OFLOW_STEM_SINGLE_A=0: the double buffer, for A/B).
-  constexpr bool ADB = (T == 1) && !(AIN == kInImg && OFLOW_STEM_SINGLE_A);
+  // input windows (the stem's image, convf1's flow): the patch operand is built per tile from a window staged in LDS
+  constexpr bool WIN = AIN == kInImg || AIN == kInFlow;
+  constexpr int WC = AIN == kInFlow ? 2 : kImgC, WS = AIN == kInFlow ? 1 : 2;  // window channels, stride
+  constexpr int WROWS = (kTY - 1) * WS + kImgK, WCOLS = (kTX - 1) * WS + kImgK;
+  // stride 2: [c][row][column parity][column / 2] (kImgHalf); stride 1: [c][row][column]
+  constexpr int WHALF = WS == 2 ? (WCOLS + 1) / 2 : WCOLS, WPITCH = WS == 2 ? 2 * WHALF : WCOLS;
+  constexpr int WPLANE = WROWS * WPITCH;
+  constexpr int WKPAD = AIN == kInFlow ? 128 : 160;  // patch channels staged (>= 49 * WC: zeros past it)
+  static_assert(AIN != kInImg || (WHALF == kImgHalf && WPITCH == kImgPitch && WPLANE == kImgPlane), "stem window");
+  constexpr bool ADB = (T == 1) && !(WIN && OFLOW_STEM_SINGLE_A);
   // 128-B LDS rows, 16-B slots XOR-swizzled (slot ^= (row >> 1) & 7): the 32 rows of an MFMA operand read by
   // ds_read_b128 are bank-conflict free from any starting row (padded 144-B rows with affine addressing measured the
   // same speed, tools/exp/conv_s32_dma.hip's history)
@@ -231,13 +241,13 @@ __global__ __launch_bounds__(64 * WM * WN, WM * WN == 8 ? 1 : 2) void conv_s32_k
   constexpr int TS = BN + 4;              // epilogue tile row stride (floats)
   constexpr int EPI_BYTES = BM * TS * 4;
   constexpr int LDS_BYTES = MAIN_BYTES > EPI_BYTES ? MAIN_BYTES : EPI_BYTES;
-  // kInImg: the stem's input window [c][row][col] + one zero float, then the patch channels' window offsets
-  constexpr int kImgZero = kImgC * kImgPlane;
+  // windows: the input window + one zero float, then the patch channels' window offsets
+  constexpr int kImgZero = WC * WPLANE;
   constexpr int IMG_FLOATS = (kImgZero + 1 + 3) & ~3;
   constexpr int AFF_BYTES = AIN == kInF32Norm ? kAinGroups * 32 * 8  // float2 (scale, shift) per input channel
-                            : AIN == kInImg ? IMG_FLOATS * 4 + 160 * 4
+                            : WIN ? IMG_FLOATS * 4 + WKPAD * 4
                             : 0;
-  static_assert(AIN != kInImg || (T == 1 && TY == kTY), "image input: 1x1 geometry over the patch channels, 4-row tiles");
+  static_assert(!WIN || (T == 1 && TY == kTY), "window input: 1x1 geometry over the patch channels, 4-row tiles");
   __shared__ __attribute__((aligned(16))) uint8_t smem[LDS_BYTES + AFF_BYTES];
   // the block's per-channel (inverse weight scale, bias), staged once for the epilogue (whose loops would otherwise
   // wait on a global-load round trip per iteration)
@@ -246,7 +256,7 @@ __global__ __launch_bounds__(64 * WM * WN, WM * WN == 8 ? 1 : 2) void conv_s32_k
   __shared__ float3 sStat[EPI == 0 ? WM * BN : 1];
   float2* sAff = reinterpret_cast<float2*>(smem + LDS_BYTES);
   float* sImg = reinterpret_cast<float*>(smem + LDS_BYTES);  // kInImg: [c][row][parity][col/2], zero at kImgZero
-  int* sKoff = reinterpret_cast<int*>(smem + LDS_BYTES + (AIN == kInImg ? IMG_FLOATS * 4 : 0));
+  int* sKoff = reinterpret_cast<int*>(smem + LDS_BYTES + (WIN ? IMG_FLOATS * 4 : 0));
   uint8_t* sA = smem;
   uint8_t* sB = smem + (ADB ? 2 : 1) * A_BYTES;
 
@@ -322,7 +332,7 @@ __global__ __launch_bounds__(64 * WM * WN, WM * WN == 8 ? 1 : 2) void conv_s32_k
 #pragma unroll
   for (int s_ = 0; s_ < BPER; ++s_) boff[s_] = (n0 + (tid + s_ * NTH) / 8) * 128 + ((tid + s_ * NTH) & 7) * 16;
 #define OFLOW_LOAD_A(RA, G)                                                                                          \
-  if constexpr (AIN != kInImg) _Pragma("unroll") for (int s_ = 0; s_ < APER; ++s_) {                                 \
+  if constexpr (!WIN) _Pragma("unroll") for (int s_ = 0; s_ < APER; ++s_) {                                        \
     int col_;                                                                                                        \
     const int off_ = a_off(s_, col_);                                                                                \
     if constexpr (AIN == kInF32) /* rows of cin floats: channels past cin re-read the row's last 16 B (zeroed) */   \
@@ -342,15 +352,15 @@ __global__ __launch_bounds__(64 * WM * WN, WM * WN == 8 ? 1 : 2) void conv_s32_k
     const int item = tid + s_ * NTH;                                                                            \
     /* image input: consecutive lanes take consecutive pixels of one chunk (conflict-free window reads); else the   \
        8 chunks of a pixel (whole 128-B LDS rows per 8 lanes) */                                                     \
-    const int p = AIN == kInImg ? item % BM : item >> 3, c = AIN == kInImg ? item / BM : item & 7;                   \
+    const int p = WIN ? item % BM : item >> 3, c = WIN ? item / BM : item & 7;                                       \
     if (AITEMS % NTH == 0 || item < AITEMS) {                                                                   \
       if constexpr (AIN != kInS32) {                                                                                 \
         /* 4 fp32 channels (G*32 + 4c ..) [-> relu(x * scale + shift)] -> 4 hi + 4 lo halves (8 B each) */           \
         typedef _Float16 half4_ __attribute__((ext_vector_type(4)));                                                 \
         half4_ h4 = {0, 0, 0, 0}, l4 = {0, 0, 0, 0};                                                                 \
-        if constexpr (AIN == kInImg) {                                                                               \
-          /* patch channel k of pixel p = the staged window at (2*py, 2*px) + the channel's table offset */          \
-          const int pb_ = 2 * (p >> 5) * kImgPitch + (p & 31);                                                       \
+        if constexpr (WIN) {                                                                                         \
+          /* patch channel k of pixel p = the staged window at (WS*py, WS*px) + the channel's table offset */        \
+          const int pb_ = WS * (p >> 5) * WPITCH + (p & 31);                                                         \
           const int4 ko_ = *reinterpret_cast<const int4*>(sKoff + (G) * 32 + 4 * c);                                 \
           const int kov_[4] = {ko_.x, ko_.y, ko_.z, ko_.w};                                                          \
           float mx_ = 0.f, v4_[4];                                                                                   \
@@ -485,11 +495,40 @@ __global__ __launch_bounds__(64 * WM * WN, WM * WN == 8 ? 1 : 2) void conv_s32_k
     for (int s_ = 0; s_ < IMG_PER; ++s_)
       if (tid + s_ * NTH < IMG_N) sImg[io[s_]] = iv[s_];
     }
-    // patch channel k = t*3 + ch, t = ky*7 + kx -> window offset ch*(rows*cols) + ky*cols + kx (-1: zero, k >= 147)
-    for (int k = tid; k < 160; k += NTH) {
-      const int t = k / kImgC, ch = k - t * kImgC;
+  }
+  if constexpr (AIN == kInFlow) {
+    // convf1's input: the tile's flow window (rows ty0 - 3 .., columns tx0 - 3 ..) from coords1 (B, 2, H, W):
+    // flow = coords1 - (x, y) as oflow_flow_prep_s32 forms it (raft.py:129), zeros outside the image (padding=3);
+    // every load issued before the first LDS store
+    const float* co = reinterpret_cast<const float*>(a.x) + (long long)b * 2 * a.H * a.W;
+    const int iy0 = ty0 - kImgK / 2, ix0 = tx0 - kImgK / 2;
+    constexpr int FL_N = 2 * WROWS * WCOLS, FL_PER = (FL_N + NTH - 1) / NTH;
+    float iv[FL_PER];
+    int io[FL_PER];
+#pragma unroll
+    for (int s_ = 0; s_ < FL_PER; ++s_) {
+      const int e = min(tid + s_ * NTH, FL_N - 1);
+      const int ch = e / (WROWS * WCOLS), rem = e - ch * (WROWS * WCOLS);
+      const int ry = rem / WCOLS, rx = rem - ry * WCOLS;
+      const int iy = iy0 + ry, ix = ix0 + rx;
+      const bool in = static_cast<unsigned>(iy) < static_cast<unsigned>(a.H) && static_cast<unsigned>(ix) < static_cast<unsigned>(a.W);
+      const int cy = min(max(iy, 0), a.H - 1), cx = min(max(ix, 0), a.W - 1);
+      const float v = co[((long long)ch * a.H + cy) * a.W + cx] - static_cast<float>(ch == 0 ? ix : iy);
+      iv[s_] = in ? v : 0.f;
+      io[s_] = ch * WPLANE + ry * WPITCH + rx;
+    }
+#pragma unroll
+    for (int s_ = 0; s_ < FL_PER; ++s_)
+      if (tid + s_ * NTH < FL_N) sImg[io[s_]] = iv[s_];
+  }
+  if constexpr (WIN) {
+    // patch channel k = t*WC + ch, t = ky*7 + kx -> window offset (-1: zero, k >= 49 * WC)
+    for (int k = tid; k < WKPAD; k += NTH) {
+      const int t = k / WC, ch = k - t * WC;
       const int ky = t / kImgK, kx = t - ky * kImgK;
-      sKoff[k] = t < kImgK * kImgK ? ch * kImgPlane + ky * kImgPitch + (kx & 1) * kImgHalf + (kx >> 1) : -1;
+      sKoff[k] = t < kImgK * kImgK
+                     ? ch * WPLANE + ky * WPITCH + (WS == 2 ? (kx & 1) * WHALF + (kx >> 1) : kx)
+                     : -1;
     }
     if (tid == 0) sImg[kImgZero] = 0.f;
     __syncthreads();
@@ -1019,6 +1058,12 @@ int launch_conv(const ConvArgs& a0, hipStream_t s) {
       return launch_status();
     }
   }
+  if constexpr (KH == 1 && KW == 1 && EPI == 0 && BN == 128 && TY == kTY) {  // convf1 from coords1's flow window
+    if (a.ain == kInFlow) {
+      hipLaunchKernelGGL((conv_s32_kernel<KH, KW, BN, WM, WN, EPI, TY, kInFlow>), grid, dim3(64 * WM * WN), 0, s, a);
+      return launch_status();
+    }
+  }
   if constexpr (KH == 1 && KW == 1 && EPI == 0 && BN == 128) {  // convc1 on the NHWC corr lookup
     if (a.ain == kInF32) {
       hipLaunchKernelGGL((conv_s32_kernel<KH, KW, BN, WM, WN, EPI, TY, kInF32>), grid, dim3(64 * WM * WN), 0, s, a);
@@ -1232,7 +1277,14 @@ extern "C" int oflow_conv_s32_ex4(const void* d_x, long long x_pixel_stride, int
     if (n_pad % 32) return OFLOW_E_SHAPE;
     a.wf = static_cast<const uint8_t*>(d_wfrag);
   }
-  if (in_format < kInS32 || in_format > kInImg) return OFLOW_E_MODE;
+  if (in_format < kInS32 || in_format > kInFlow) return OFLOW_E_MODE;
+  if (in_format == kInFlow) {  // convf1 from coords1: 1x1 geometry over 4 patch groups, BN 128, epilogue 0
+    if (kh != 1 || kw != 1 || epilogue != 0 || block_n != 128 || in_groups != (kImgK * kImgK * 2 + 31) / 32)
+      return OFLOW_E_MODE;
+    if ((long long)2 * B * H * W >= (1ll << 31) || d_addend) return OFLOW_E_SHAPE;
+    a.ain = in_format;
+    return dispatch_conv(a, kh, kw, block_n, epilogue, static_cast<hipStream_t>(stream));
+  }
   if (in_format == kInImg) {  // the stem from the image: 1x1 geometry over 5 patch groups, BN 64, epilogue 0
     if (kh != 1 || kw != 1 || epilogue != 0 || block_n != 64 || in_groups != (kImgK * kImgK * kImgC + 31) / 32)
       return OFLOW_E_MODE;

@@ -157,7 +157,7 @@ __global__ __launch_bounds__(256) void flow_prep_tiled_kernel(const float* __res
   // of the group's values 8c .. 8c+7 (taps 16g + 4c .. +3, x and y), c >= 4 the lo halves of values 8(c-4) ..
   float gm = 0.f;
 #pragma unroll 4
-  for (int i = 0; i < (kFpTH * kFpTW * G * 8) / 256; ++i) {
+  for (int i = 0; i < (pm ? (kFpTH * kFpTW * G * 8) / 256 : 0); ++i) {
     const int k = threadIdx.x + 256 * i, line = k >> 3, c = k & 7;
     const int pl = line >> 2, g = line & 3, py = pl / kFpTW, px = pl - py * kFpTW;
     const int y = ty0 + py, x = tx0 + px;
@@ -180,6 +180,10 @@ __global__ __launch_bounds__(256) void flow_prep_tiled_kernel(const float* __res
   }
   range_guard(gm);  // (the centre tap is among the patch values: the flow channels below are covered)
   const int pl = threadIdx.x & (kFpTH * kFpTW - 1), py = pl / kFpTW, px = pl - py * kFpTW;
+  if (!pm && threadIdx.x < 128) {  // no patch matrix: guard the flow channels themselves
+    const float2 f = sF[(py + 3) * kFpWW + px + 3];
+    if (ty0 + py < H && tx0 + px < W) range_guard(fmaxf(fabsf(f.x), fabsf(f.y)));
+  }
   const int y = ty0 + py, x = tx0 + px;
   if (y >= H || x >= W) return;
   const long long p = (long long)b * HW + (long long)y * W + x;
@@ -457,7 +461,8 @@ extern "C" void oflow_exp_set_flow_prep_untiled(int on) { oflow::g_flow_prep_unt
 extern "C" int oflow_flow_prep_s32(const float* d_coords, int B, int H, int W, void* d_patches, void* d_flow0,
                                    long long flow0_pixel_stride, void* d_flow1, long long flow1_pixel_stride,
                                    void* stream) {
-  if (!d_coords || !d_patches) return OFLOW_E_NULL;
+  // d_patches may be null (only the flow channels: convf1 then reads coords1 itself, OFLOW_IN_FLOW7)
+  if (!d_coords || (!d_patches && !d_flow0) || (!d_patches && g_flow_prep_untiled)) return OFLOW_E_NULL;
   if (B <= 0 || H <= 0 || W <= 0) return OFLOW_E_SHAPE;
   if (((uintptr_t)d_patches & 15) || (d_flow0 && ((uintptr_t)d_flow0 & 3)) || (d_flow1 && ((uintptr_t)d_flow1 & 3)))
     return OFLOW_E_ALIGN;

@@ -9,6 +9,7 @@ is not provided.
 """
 from __future__ import annotations
 
+import os
 from typing import Optional, Tuple
 
 import torch
@@ -28,6 +29,10 @@ CONV_BN = {"c2": 64, "f1": 128, "f2": 64, "mo": 128, "gru": 128, "fh1": 128}
 # of the 8-pair step: col2im 19.99 / 19.85 ms (median / min) vs conv 19.93 / 19.74 (profiles/r04/s2_ab_fh.log): in the
 # step the other pair lane fills the CUs the 2-column conv leaves idle, so "conv" stays the default
 FLOW_HEAD_MODE = "conv"
+# convf1 (7x7, 2 -> 128) straight from coords1 (_native.FlowIn, OFLOW_IN_FLOW7: each tile stages its flow window and
+# builds the patch operand in LDS) from this many pixels of the whole forward's batch up; below it flow_prep writes the
+# patch matrix and convf1 runs on the small-grid tiles. Bit-identical either way (same patch values, same k order).
+CONVF1_FROM_FLOW_MIN_PIXELS = 16384 if os.environ.get("OFLOW_CONVF1_FROM_FLOW", "1") != "0" else 1 << 62  # (0: A/B)
 
 class FlowHead(nn.Module):
     def __init__(self, input_dim: int = 128, hidden_dim: int = 256) -> None:
@@ -282,6 +287,7 @@ class SplitUpdate:
         # from the pixel count of the WHOLE forward's batch so that pair lanes give the single-lane results bit for bit
         px = b * h * w if flow_head_pixels is None else int(flow_head_pixels)
         self.flow_head_fma = px < _native.FLOW_HEAD2_MAX_PIXELS
+        self.f1_from_flow = px >= CONVF1_FROM_FLOW_MIN_PIXELS
         S = _native.s32_empty
         self.hx = S(b, h, w, 8, dev)
         self.rhx = S(b, h, w, 8, dev)
@@ -290,7 +296,7 @@ class SplitUpdate:
         self.corr_f32 = None  # [B*H*W, corr_ch], allocated on first use
         self.c1 = S(b, h, w, 8, dev)
         self.cf = S(b, h, w, 8, dev)
-        self.pm = S(b, h, w, 4, dev)
+        self.pm = None if self.f1_from_flow else S(b, h, w, 4, dev)  # convf1's patch matrix (small grids only)
         self.f1 = S(b, h, w, 4, dev)
         self.fh = S(b, h, w, 8, dev)
         self.fh2y = None  # (B, 18, H, W) per-tap products of the flow head's output conv (flow_head_mode "col2im")
@@ -401,11 +407,12 @@ class SplitUpdate:
         # group is read again only after the join).
         main = torch.cuda.current_stream(coords1.device)
         side = self.side_stream if self.streams else None
+        f1_in = V(self.pm) if self.pm is not None else _native.FlowIn(coords1)
         if side is not None:
             side.wait_stream(main)
             with torch.cuda.stream(side):
                 _native.flow_prep(coords1, self.pm, (V(self.hx), 254), (V(self.rhx), 254))
-                conv(V(self.pm), w["f1"], CONV_BN["f1"], "relu", y0=V(self.f1))
+                conv(f1_in, w["f1"], CONV_BN["f1"], "relu", y0=V(self.f1))
                 conv(V(self.f1), w["f2"], CONV_BN["f2"], "relu", y0=V(self.cf, 6, 2))
             self._convc1(corr_in)
             conv(V(self.c1), w["c2"], CONV_BN["c2"], "relu", y0=V(self.cf, 0, 6))
@@ -414,7 +421,7 @@ class SplitUpdate:
             _native.flow_prep(coords1, self.pm, (V(self.hx), 254), (V(self.rhx), 254))
             self._convc1(corr_in)
             conv(V(self.c1), w["c2"], CONV_BN["c2"], "relu", y0=V(self.cf, 0, 6))
-            conv(V(self.pm), w["f1"], CONV_BN["f1"], "relu", y0=V(self.f1))
+            conv(f1_in, w["f1"], CONV_BN["f1"], "relu", y0=V(self.f1))
             conv(V(self.f1), w["f2"], CONV_BN["f2"], "relu", y0=V(self.cf, 6, 2))
         conv(V(self.cf), w["mo"], CONV_BN["mo"], "relu", y0=V(self.hx, 4, 4), y1=V(self.rhx, 4, 4))
         for tag, gx in zip(("1", "2"), self.gx):

@@ -11,7 +11,7 @@ from __future__ import annotations
 
 import ctypes
 import os
-from typing import List, Sequence
+from typing import List, Optional, Sequence
 
 import torch
 
@@ -831,6 +831,37 @@ class ImgIn:
         return self.raw.device
 
 
+class FlowIn:
+    """convf1's input given as coords1 (B, 2, H, W) fp32 itself (OFLOW_IN_FLOW7): flow = coords1 - the pixel grid
+    and its 7x7 pad-3 patch operand are built per output tile from a staged window, so no patch matrix is written or
+    read. For ConvWeights packed with ``patches=True`` (4 groups); bit-identical to the conv of flow_prep's matrix."""
+
+    __slots__ = ("raw", "bhw")
+    in_format = 4
+
+    def __init__(self, coords: torch.Tensor):
+        if coords.dtype != torch.float32 or coords.dim() != 4 or coords.shape[1] != 2 or not coords.is_contiguous():
+            raise RuntimeError("FlowIn: coords must be contiguous fp32 (B, 2, H, W)")
+        b, _, hh, ww = coords.shape
+        self.raw, self.bhw = coords, (int(b), int(hh), int(ww))
+
+    @property
+    def ptr(self) -> int:
+        return self.raw.data_ptr()
+
+    @property
+    def ps(self) -> int:
+        return 0
+
+    @property
+    def ng(self) -> int:
+        return 4
+
+    @property
+    def device(self):
+        return self.raw.device
+
+
 class NhwcNormIn:
     """Convolution input given as the previous convolution's raw fp32 NHWC output [B*H*W, C] plus its instance-norm
     affine (scale, shift: [B, C]); the kernel stages relu(raw * scale + shift) (oflow_conv_s32_ex2), so the normalised
@@ -1215,17 +1246,21 @@ def replicate_pad(inputs, pad):
     return outs
 
 
-def flow_prep(coords: torch.Tensor, patches: torch.Tensor, flow0=None, flow1=None) -> None:
-    """coords1 (B, 2, H, W) -> convf1 patch matrix (S32, 4 groups) and the flow channels of the GRU inputs.
-    flow0/flow1: (S32Slice, channel) pairs naming where the x flow channel lives (y follows it)."""
+def flow_prep(coords: torch.Tensor, patches: Optional[torch.Tensor], flow0=None, flow1=None) -> None:
+    """coords1 (B, 2, H, W) -> convf1 patch matrix (S32, 4 groups; None: not written, convf1 reading coords1 through
+    ``FlowIn``) and the flow channels of the GRU inputs. flow0/flow1: (S32Slice, channel) pairs naming where the x flow
+    channel lives (y follows it)."""
     co = _gpu_f32(coords, "coords", "flow_prep")
     b, _, h, w = co.shape
-    if tuple(patches.shape) != (b, h, w, 4, 2, 32) or patches.dtype != torch.float16:
+    if patches is None and flow0 is None:
+        raise RuntimeError("flow_prep: nothing to write")
+    if patches is not None and (tuple(patches.shape) != (b, h, w, 4, 2, 32) or patches.dtype != torch.float16):
         raise RuntimeError("flow_prep: patches must be S32 (B, H, W, 4, 2, 32)")
     f0 = (flow0[0].channel_ptr(flow0[1]), flow0[0].ps) if flow0 is not None else (None, 0)
     f1 = (flow1[0].channel_ptr(flow1[1]), flow1[0].ps) if flow1 is not None else (None, 0)
     with torch.cuda.device(co.device), _Timed("flow_prep", co.device):
-        _check(load().oflow_flow_prep_s32(co.data_ptr(), b, h, w, patches.data_ptr(), f0[0], f0[1], f1[0], f1[1], _stream(co.device)), "flow_prep")
+        _check(load().oflow_flow_prep_s32(co.data_ptr(), b, h, w, patches.data_ptr() if patches is not None else None,
+                                          f0[0], f0[1], f1[0], f1[1], _stream(co.device)), "flow_prep")
 
 
 def corr_lookup_backward(grad_out: torch.Tensor, coords: torch.Tensor, radius: int, level0_hw, num_levels: int):
