@@ -236,6 +236,12 @@ int oflow_timing_event_elapsed_ms(void* start, void* end, float* ms);
 
 int oflow_flow_head2_s32(const void* d_x, long long x_pixel_stride, int in_groups, const float* d_weight,
                          const float* d_bias, int B, int H, int W, float* d_coords, void* stream);
+/* oflow_flow_head2_tiled_s32: oflow_flow_head2_s32 for large grids (update.py:36 FlowHead.conv2 + raft.py:133): each
+ * workgroup stages a 4 x 32 output tile's 6 x 34 halo per 32-channel group in LDS as fp32 (hi + lo) and runs the
+ * 3x3 x C -> 2 products as fp32 FMAs. d_wr: the weight (2, C, 3, 3) repacked [group][4-channel chunk][tap][output][4]
+ * (16-B aligned); coords1 (B, 2, H, W) += conv + bias. */
+int oflow_flow_head2_tiled_s32(const void* d_x, long long x_pixel_stride, int in_groups, const float* d_wr,
+                               const float* d_bias, int B, int H, int W, float* d_coords, void* stream);
 /* oflow_corr_lookup_tiled_nhwc_f32: the tiled lookup as fp32 NHWC rows [B*H*W][row_floats] (d_out 16-B aligned) in the
  * reference's channel order: row q, channel l*(2r+1)^2 + k = oflow_corr_lookup_tiled_f32's (b, l*(2r+1)^2 + k, y, x) bit for
  * bit; row_floats >= num_levels*(2r+1)^2, channels past that are not written. With row_floats = num_levels*(2r+1)^2 (324)

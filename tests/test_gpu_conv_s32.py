@@ -424,10 +424,12 @@ def test_range_check_fires_on_fp16_overflow(monkeypatch):
     N.conv_s32(N.S32Slice(N.s32_from_f32(big)), cw, 32, f32=out)  # off: no check, no raise
 
 
-@pytest.mark.parametrize("b,h,w", [(2, 55, 128), (1, 7, 9), (3, 16, 33)])
-def test_flow_head2_matches_fp64(b, h, w):
-    """The flow head's 2-channel output conv as fp32 FMAs (oflow_flow_head2_s32) added into coords, vs float64; the
-    small grids put most pixels on the zero-padded border."""
+@pytest.mark.parametrize("tiled", [False, True])
+@pytest.mark.parametrize("b,h,w", [(2, 55, 128), (1, 7, 9), (3, 16, 33), (4, 55, 128)])
+def test_flow_head2_matches_fp64(b, h, w, tiled):
+    """The flow head's 2-channel output conv as fp32 FMAs (oflow_flow_head2_s32, and the LDS-tiled large-grid form
+    oflow_flow_head2_tiled_s32) added into coords, vs float64; the small grids put most pixels on the zero-padded
+    border, ragged tiles included."""
     g = torch.Generator().manual_seed(h * w)
     x = (torch.randn(b, 256, h, w, generator=g) * 1.5).to(DEV)
     wt = (torch.randn(2, 256, 3, 3, generator=g) / 48.0).to(DEV)
@@ -437,7 +439,10 @@ def test_flow_head2_matches_fp64(b, h, w):
     coords = torch.randn(b, 2, h, w, generator=g).to(DEV)
     ref = coords.double() + F.conv2d(xr.double(), wt.double(), bias.double(), padding=1)
     bound = F.conv2d(xr.double().abs(), wt.double().abs(), None, padding=1)
-    N.flow_head2(N.S32Slice(xs), wt.contiguous(), bias, coords)
+    if tiled:
+        N.flow_head2_tiled(N.S32Slice(xs), N.flow_head2_tiled_weights(wt), bias, coords)
+    else:
+        N.flow_head2(N.S32Slice(xs), wt.contiguous(), bias, coords)
     torch.cuda.synchronize()
     err = (coords.double() - ref).abs()
     tol = 2e-6 * bound + 1e-6 + 2.0 ** -23 * ref.abs()

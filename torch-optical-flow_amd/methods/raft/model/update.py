@@ -28,7 +28,7 @@ CONV_BN = {"c2": 64, "f1": 128, "f2": 64, "mo": 128, "gru": 128, "fh1": 128}
 # pixel, 18 of 32 MFMA columns used) + a gather of the 9 taps into coords1 (oflow_flow_head_col2im_f32). In-process A/B
 # of the 8-pair step: col2im 19.99 / 19.85 ms (median / min) vs conv 19.93 / 19.74 (profiles/r04/s2_ab_fh.log): in the
 # step the other pair lane fills the CUs the 2-column conv leaves idle, so "conv" stays the default
-FLOW_HEAD_MODE = "conv"
+FLOW_HEAD_MODE = os.environ.get("OFLOW_FLOW_HEAD_MODE", "conv")
 # convf1 (7x7, 2 -> 128) straight from coords1 (_native.FlowIn, OFLOW_IN_FLOW7: each tile stages its flow window and
 # builds the patch operand in LDS) from this many pixels of the whole forward's batch up; below it flow_prep writes the
 # patch matrix and convf1 runs on the small-grid tiles. Bit-identical either way (same patch values, same k order).
@@ -348,6 +348,8 @@ class SplitUpdate:
             "fh2_bias": fh.conv2.bias.detach().float().contiguous(),
             # small grids: the 2-channel output conv as fp32 FMAs (oflow_flow_head2_s32) on the conv's own weights
             "fh2_f32": (fh.conv2.weight.detach().float().contiguous(), fh.conv2.bias.detach().float().contiguous()),
+            # large grids: the same as fp32 FMAs on an LDS-staged halo (oflow_flow_head2_tiled_s32), repacked weights
+            "fh2_tiled": (_native.flow_head2_tiled_weights(fh.conv2.weight), fh.conv2.bias.detach().float().contiguous()),
             "m1": CW(block.mask[0].weight, block.mask[0].bias, 256),
             "m2": CW(block.mask[2].weight, block.mask[2].bias, 576),
         }
@@ -433,6 +435,8 @@ class SplitUpdate:
         conv(net, w["fh1"], CONV_BN["fh1"], "relu", y0=V(self.fh))
         if self.flow_head_fma and coords1.is_contiguous():
             _native.flow_head2(V(self.fh), *w["fh2_f32"], coords1)  # coords1 += conv2(.) (raft.py:133)
+        elif self.flow_head_mode == "tiled" and coords1.is_contiguous():
+            _native.flow_head2_tiled(V(self.fh), *w["fh2_tiled"], coords1)  # coords1 += conv2(.) (raft.py:133)
         elif self.flow_head_mode == "col2im" and coords1.is_contiguous():
             if self.fh2y is None:
                 self.fh2y = torch.empty((b, 18, h, wd), device=coords1.device, dtype=torch.float32)

@@ -67,6 +67,7 @@ SYMBOLS = (
     "oflow_corr_lookup_convc1_s32",
     "oflow_corr_pyramid_tiled_s32",
     "oflow_flow_head2_s32",
+    "oflow_flow_head2_tiled_s32",
     "oflow_conv_s32_ex3",
     "oflow_conv_s32_ex4",
     "oflow_normalize_images_f32",
@@ -254,6 +255,8 @@ def load() -> ctypes.CDLL:
     lib.oflow_convex_upsample_f32.restype = I
     lib.oflow_flow_head2_s32.restype = I
     lib.oflow_flow_head2_s32.argtypes = [P, ctypes.c_longlong, I, P, P, I, I, I, P, P]
+    lib.oflow_flow_head2_tiled_s32.restype = I
+    lib.oflow_flow_head2_tiled_s32.argtypes = [P, ctypes.c_longlong, I, P, P, I, I, I, P, P]
     lib.oflow_corr_pyramid_tiled_s32.restype = I
     lib.oflow_corr_pyramid_tiled_s32.argtypes = [P, P, I, I, I, I, I, PP, P]
     lib.oflow_corr_lookup_convc1_s32.restype = I
@@ -1122,6 +1125,34 @@ def flow_head2(x: "S32Slice", weight: torch.Tensor, bias: torch.Tensor, coords: 
     with torch.cuda.device(coords.device), _Timed("conv3x3", coords.device):
         _check(load().oflow_flow_head2_s32(x.ptr, x.ps, x.ng, weight.data_ptr(), bias.data_ptr(), b, h, w,
                                            coords.data_ptr(), _stream(coords.device)), what)
+
+
+def flow_head2_tiled_weights(weight: torch.Tensor) -> torch.Tensor:
+    """(2, C, 3, 3) fp32 -> the [group][4-channel chunk][tap][output][4] copy oflow_flow_head2_tiled_s32 reads."""
+    o, c = weight.shape[:2]
+    if o != 2 or c % 32 or tuple(weight.shape[2:]) != (3, 3):
+        raise RuntimeError("flow_head2_tiled_weights: weight must be (2, C, 3, 3) with C a multiple of 32")
+    w = weight.detach().float().reshape(2, c // 32, 8, 4, 3, 3)  # o, g, c4, e, ky, kx
+    return w.permute(1, 2, 4, 5, 0, 3).contiguous()  # g, c4, ky, kx, o, e
+
+
+def flow_head2_tiled(x: "S32Slice", wr: torch.Tensor, bias: torch.Tensor, coords: torch.Tensor) -> None:
+    """coords += conv3x3(x, weight, bias) for the flow head's 2-channel output conv as fp32 FMAs on an LDS-staged halo
+    (oflow_flow_head2_tiled_s32; update.py:36, raft.py:133), the large-grid form. wr: flow_head2_tiled_weights(weight)."""
+    what = "flow_head2_tiled"
+    b, h, w = x.bhw
+    if wr.dtype != torch.float32 or not wr.is_contiguous() or wr.numel() != 2 * x.ng * 32 * 9 or wr.data_ptr() % 16:
+        raise RuntimeError(f"{what}: wr must be flow_head2_tiled_weights of a (2, {x.ng * 32}, 3, 3) weight")
+    if bias is None or bias.dtype != torch.float32 or tuple(bias.shape) != (2,):
+        raise RuntimeError(f"{what}: bias must be fp32 (2,)")
+    if coords.dtype != torch.float32 or not coords.is_contiguous() or tuple(coords.shape) != (b, 2, h, w):
+        raise RuntimeError(f"{what}: coords must be contiguous fp32 ({b}, 2, {h}, {w})")
+    if _flops is not None:
+        fl = 2 * b * h * w * 2 * x.ng * 32 * 9
+        _count(0, fl, fl)
+    with torch.cuda.device(coords.device), _Timed("conv3x3", coords.device):
+        _check(load().oflow_flow_head2_tiled_s32(x.ptr, x.ps, x.ng, wr.data_ptr(), bias.data_ptr(), b, h, w,
+                                                 coords.data_ptr(), _stream(coords.device)), what)
 
 
 def flow_head_col2im(y: torch.Tensor, bias: torch.Tensor, coords: torch.Tensor) -> None:
