@@ -28,7 +28,10 @@ CONV_BN = {"c2": 64, "f1": 128, "f2": 64, "mo": 128, "gru": 128, "fh1": 128}
 # pixel, 18 of 32 MFMA columns used) + a gather of the 9 taps into coords1 (oflow_flow_head_col2im_f32). In-process A/B
 # of the 8-pair step: col2im 19.99 / 19.85 ms (median / min) vs conv 19.93 / 19.74 (profiles/r04/s2_ab_fh.log): in the
 # step the other pair lane fills the CUs the 2-column conv leaves idle, so "conv" stays the default
-FLOW_HEAD_MODE = os.environ.get("OFLOW_FLOW_HEAD_MODE", "conv")
+# r05: "tiled" = oflow_flow_head2_tiled_s32 (fp32 FMAs on an LDS-staged halo, 512 threads per 4 x 32 tile): step A/B
+# 18.81 vs 18.89 ms against "conv" (profiles/r05/s33_flow_head_tiled_ab.log; the first 256-thread form was 0.25 ms
+# slower, s32): the default
+FLOW_HEAD_MODE = os.environ.get("OFLOW_FLOW_HEAD_MODE", "tiled")
 # convf1 (7x7, 2 -> 128) straight from coords1 (_native.FlowIn, OFLOW_IN_FLOW7: each tile stages its flow window and
 # builds the patch operand in LDS) from this many pixels of the whole forward's batch up; below it flow_prep writes the
 # patch matrix and convf1 runs on the small-grid tiles. Bit-identical either way (same patch values, same k order).
