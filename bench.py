@@ -386,8 +386,8 @@ def main() -> int:
     if args.graph and args.eager:
         print("bench: --graph and --eager exclude each other", file=sys.stderr)
         return 2
-    # graph replay by default for the RAFT workloads (one capture per rank; a second step in flight would share its
-    # static buffers, so --inflight > 1 stays eager)
+    # graph replay by default for the RAFT workloads (one capture per rank; with --graph --inflight N, N captures,
+    # step i replaying capture i %% N on stream i %% N: each capture owns its static buffers)
     args.graph = args.graph or (not args.eager and args.workload in ("sintel", "kitti") and args.inflight == 1
                                 and args.update_impl == "split")
 
@@ -468,11 +468,18 @@ def main() -> int:
         # per-kernel timing inside the graph: native event-record nodes captured around the timed launches, re-recorded
         # by every replay (read after the timed region: they time its last replay)
         graph_rec = None if args.no_events else ({"_native": True, "*": True} if args.conv_events else {"_native": True})
+        # one capture per step in flight (the first holds the timing nodes); fwd() replays them in turn, and issue(i)
+        # runs step i on stream i % inflight, so consecutive replays of one capture stay ordered on one stream
+        ngraphs = max(1, args.inflight) if world == 1 else 1
         with torch.inference_mode():
-            graphed = GraphedRAFT(model, pp[0], pp[1], iters=iters, recorder=graph_rec)
+            graphs = [GraphedRAFT(model, pp[0], pp[1], iters=iters, recorder=graph_rec if g == 0 else None)
+                      for g in range(ngraphs)]
+        gturn = [0]
 
         def fwd(s0, s1):
             p0, p1 = padder.pad(s0, s1)
+            graphed = graphs[gturn[0] % ngraphs]
+            gturn[0] += 1
             low, up = graphed(p0, p1)
             if world > 1:
                 # the graph's outputs are overwritten by the next replay, while this step's gathers may still be
@@ -507,7 +514,10 @@ def main() -> int:
         return out
 
     with torch.inference_mode():
-        run_steps(max(args.warmup, 1 if pipelined else len(streams)))
+        nwarm = max(args.warmup, 1 if pipelined else len(streams))
+        if args.graph and not pipelined:
+            nwarm = -(-nwarm // len(streams)) * len(streams)  # the timed steps start at stream 0 / capture 0
+        run_steps(nwarm)
         torch.cuda.synchronize(dev)
         # graph replays launch no Python: their per-kernel events are the graph's own nodes (graph_rec, captured above)
         rec = ({"*": True} if args.conv_events else {}) if not (args.no_events or args.graph) else None

@@ -287,17 +287,20 @@ __global__ __launch_bounds__(256) void replicate_pad_kernel(PadArgs a, int count
 // 4 x 32 output tile and stages, per 32-channel group, its 6 x 34 halo as fp32 (hi + lo, exact) in LDS (144-B pixel
 // stride: the 32 lanes of an output row read 16-B slots 144 B apart, conflict-free); 512 threads = 128 output pixels x
 // 4 channel quarters (8 channels of every group, two independent FMA chains per output), the weights from a
-// host-repacked [group][4-channel chunk][tap][output][4] copy through scalar loads, the next group's halo prefetched
+// host-repacked [group][4-channel chunk][tap][output][4] copy through scalar loads, the next pass's halos prefetched
 // into registers behind the FMAs; the quarters meet in LDS in a fixed order. Each input pixel is read once per tile
 // (1.6x with the halo) instead of 9 times through L1/L2 (flow_head2_kernel).
 constexpr int kF2TH = 4, kF2TW = 32, kF2HR = kF2TH + 2, kF2HC = kF2TW + 2, kF2HP = kF2HR * kF2HC, kF2PS = 9;
 constexpr int kF2NT = 512;  // threads: 128 output pixels x 4 channel quarters (8 channels of each group)
+// groups staged per pass (two halo buffers, 58.8 KB): half the barriers, and each prefetch has two groups' FMAs to
+// hide behind; same FMA order per chain as one group per pass (bit-identical)
+constexpr int kF2GP = 2;
 __global__ __launch_bounds__(kF2NT) void flow_head2_tiled_kernel(const uint8_t* __restrict__ x, long long xps, int G, int H,
                                                                  int W, int tiles_x, int tiles_y, const float* __restrict__ wr,
                                                                  const float* __restrict__ bias, float* __restrict__ coords) {
   typedef _Float16 half8_t __attribute__((ext_vector_type(8)));
   typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
-  __shared__ float4 sX[kF2HP * kF2PS];
+  __shared__ float4 sX[kF2GP][kF2HP * kF2PS];
   __shared__ float2 sPart[3][kF2TH * kF2TW];
   int t = blockIdx.x;
   const int tx0 = (t % tiles_x) * kF2TW;
@@ -307,7 +310,7 @@ __global__ __launch_bounds__(kF2NT) void flow_head2_tiled_kernel(const uint8_t* 
   const int tid = threadIdx.x, pl = tid & 127, qq = __builtin_amdgcn_readfirstlane(tid >> 7);
   const int py = pl >> 5, px = pl & 31;
   constexpr int NIT = (kF2HP * 4 + kF2NT - 1) / kF2NT;  // staging items (halo pixel, 8-channel chunk) per thread
-  u32x4_t rh[NIT], rl[NIT];
+  u32x4_t rh[kF2GP][NIT], rl[kF2GP][NIT];
   unsigned inm = 0u;  // staging items inside the image (the others load a clamped pixel and stage zeros: padding 1)
 #pragma unroll
   for (int s_ = 0; s_ < NIT; ++s_) {
@@ -316,57 +319,70 @@ __global__ __launch_bounds__(kF2NT) void flow_head2_tiled_kernel(const uint8_t* 
     const bool in = static_cast<unsigned>(hy) < static_cast<unsigned>(H) && static_cast<unsigned>(hx) < static_cast<unsigned>(W);
     inm |= (in ? 1u : 0u) << s_;
   }
-  auto load = [&](int g) {
+  auto load = [&](int g, int k) {
 #pragma unroll
     for (int s_ = 0; s_ < NIT; ++s_) {
       const int item = min(tid + kF2NT * s_, kF2HP * 4 - 1), hp = item >> 2, q = item & 3;
       const int hy = ty0 - 1 + hp / kF2HC, hx = tx0 - 1 + hp % kF2HC;
       const int cy = min(max(hy, 0), H - 1), cx = min(max(hx, 0), W - 1);
       const uint8_t* line = x + ((long long)(b * H + cy) * W + cx) * xps + g * 128 + q * 16;
-      rh[s_] = *reinterpret_cast<const u32x4_t*>(line);
-      rl[s_] = *reinterpret_cast<const u32x4_t*>(line + 64);
+      rh[k][s_] = *reinterpret_cast<const u32x4_t*>(line);
+      rl[k][s_] = *reinterpret_cast<const u32x4_t*>(line + 64);
     }
   };
   float acc[2][2] = {{0.f, 0.f}, {0.f, 0.f}};  // [channel chunk of the quarter][output]: independent FMA chains
-  load(0);
-  for (int g = 0; g < G; ++g) {
-    __syncthreads();  // every thread is done reading group g-1's halo
 #pragma unroll
-    for (int s_ = 0; s_ < NIT; ++s_) {
-      const int item = tid + kF2NT * s_;
-      if (item < kF2HP * 4) {
-        const int hp = item >> 2, q = item & 3;
-        const half8_t hv = __builtin_bit_cast(half8_t, rh[s_]), lv = __builtin_bit_cast(half8_t, rl[s_]);
-        const bool in = (inm >> s_) & 1u;
-        float f[8];
+  for (int k = 0; k < kF2GP; ++k)
+    if (k < G) load(k, k);
+  for (int g0 = 0; g0 < G; g0 += kF2GP) {
+    __syncthreads();  // every thread is done reading the previous pass's halos
 #pragma unroll
-        for (int j = 0; j < 8; ++j) f[j] = in ? static_cast<float>(hv[j]) + static_cast<float>(lv[j]) : 0.f;
-        sX[hp * kF2PS + 2 * q] = make_float4(f[0], f[1], f[2], f[3]);
-        sX[hp * kF2PS + 2 * q + 1] = make_float4(f[4], f[5], f[6], f[7]);
+    for (int k = 0; k < kF2GP; ++k) {
+      if (g0 + k >= G) break;
+#pragma unroll
+      for (int s_ = 0; s_ < NIT; ++s_) {
+        const int item = tid + kF2NT * s_;
+        if (item < kF2HP * 4) {
+          const int hp = item >> 2, q = item & 3;
+          const half8_t hv = __builtin_bit_cast(half8_t, rh[k][s_]), lv = __builtin_bit_cast(half8_t, rl[k][s_]);
+          const bool in = (inm >> s_) & 1u;
+          float f[8];
+#pragma unroll
+          for (int j = 0; j < 8; ++j) f[j] = in ? static_cast<float>(hv[j]) + static_cast<float>(lv[j]) : 0.f;
+          sX[k][hp * kF2PS + 2 * q] = make_float4(f[0], f[1], f[2], f[3]);
+          sX[k][hp * kF2PS + 2 * q + 1] = make_float4(f[4], f[5], f[6], f[7]);
+        }
       }
     }
     __syncthreads();
-    if (g + 1 < G) load(g + 1);
 #pragma unroll
-    for (int tap = 0; tap < 9; ++tap) {
-      const int ky = tap / 3, kx = tap - ky * 3;
+    for (int k = 0; k < kF2GP; ++k)
+      if (g0 + kF2GP + k < G) load(g0 + kF2GP + k, k);
 #pragma unroll
-      for (int cl = 0; cl < 2; ++cl) {
-        const int c4 = qq * 2 + cl;
-        const float4 v = sX[((py + ky) * kF2HC + px + kx) * kF2PS + c4];
-        const float4* wq = reinterpret_cast<const float4*>(wr) + ((g * 8 + c4) * 9 + tap) * 2;
-        const float4 w0 = wq[0], w1 = wq[1];
-        float a0 = acc[cl][0], a1 = acc[cl][1];
-        a0 = fmaf(v.x, w0.x, a0);
-        a0 = fmaf(v.y, w0.y, a0);
-        a0 = fmaf(v.z, w0.z, a0);
-        a0 = fmaf(v.w, w0.w, a0);
-        a1 = fmaf(v.x, w1.x, a1);
-        a1 = fmaf(v.y, w1.y, a1);
-        a1 = fmaf(v.z, w1.z, a1);
-        a1 = fmaf(v.w, w1.w, a1);
-        acc[cl][0] = a0;
-        acc[cl][1] = a1;
+    for (int k = 0; k < kF2GP; ++k) {
+      const int g = g0 + k;
+      if (g >= G) break;
+#pragma unroll
+      for (int tap = 0; tap < 9; ++tap) {
+        const int ky = tap / 3, kx = tap - ky * 3;
+#pragma unroll
+        for (int cl = 0; cl < 2; ++cl) {
+          const int c4 = qq * 2 + cl;
+          const float4 v = sX[k][((py + ky) * kF2HC + px + kx) * kF2PS + c4];
+          const float4* wq = reinterpret_cast<const float4*>(wr) + ((g * 8 + c4) * 9 + tap) * 2;
+          const float4 w0 = wq[0], w1 = wq[1];
+          float a0 = acc[cl][0], a1 = acc[cl][1];
+          a0 = fmaf(v.x, w0.x, a0);
+          a0 = fmaf(v.y, w0.y, a0);
+          a0 = fmaf(v.z, w0.z, a0);
+          a0 = fmaf(v.w, w0.w, a0);
+          a1 = fmaf(v.x, w1.x, a1);
+          a1 = fmaf(v.y, w1.y, a1);
+          a1 = fmaf(v.z, w1.z, a1);
+          a1 = fmaf(v.w, w1.w, a1);
+          acc[cl][0] = a0;
+          acc[cl][1] = a1;
+        }
       }
     }
   }

@@ -30,7 +30,7 @@ CONV_BN = {"c2": 64, "f1": 128, "f2": 64, "mo": 128, "gru": 128, "fh1": 128}
 # step the other pair lane fills the CUs the 2-column conv leaves idle, so "conv" stays the default
 # r05: "tiled" = oflow_flow_head2_tiled_s32 (fp32 FMAs on an LDS-staged halo, 512 threads per 4 x 32 tile): step A/B
 # 18.81 vs 18.89 ms against "conv" (profiles/r05/s33_flow_head_tiled_ab.log; the first 256-thread form was 0.25 ms
-# slower, s32): the default
+# slower, s32): the default; two channel groups per staging pass: +0.6 % on the graph bench (s37), bit-identical
 FLOW_HEAD_MODE = os.environ.get("OFLOW_FLOW_HEAD_MODE", "tiled")
 # convf1 (7x7, 2 -> 128) straight from coords1 (_native.FlowIn, OFLOW_IN_FLOW7: each tile stages its flow window and
 # builds the patch operand in LDS) from this many pixels of the whole forward's batch up; below it flow_prep writes the
