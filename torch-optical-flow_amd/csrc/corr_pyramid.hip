@@ -182,8 +182,22 @@ __device__ __forceinline__ void pyramid_epilogue(const PyramidArgs& p, f32x16 (&
     const int tb = p.WB[0] - (tx0 >> 3);  // tiles of this tile row that exist in the level (>= 1)
     float* const L0b = lvl_base(p, 0, (size_t)b * Nn + i0);
     __syncthreads();  // the main loop's LDS operand reads are done (the scratch aliases them)
+    // experiment (mode bit 4): level-0 stores straight from the accumulators, same addresses, unstaged values
+    const bool direct = (p.stagger_mode & 16) != 0;
 #pragma unroll
     for (int ps = 0; ps < 4; ++ps) {
+      if (direct) {
+        const int tr = lane >> 5, ch = lane & 31;
+        const int y0 = ty0 + 4 * tr;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const int i = i0 + wave * 32 + 8 * ps + j;
+          const float4 v = make_float4(acc[j][4 * ps], acc[j][4 * ps + 1], acc[j][4 * ps + 2], acc[j][4 * ps + 3]);
+          if (i < p.N && (y0 >> 2) < p.HB[0] && (ch >> 3) < tb)
+            *reinterpret_cast<float4*>(&L0b[lvl_off32(p, 0, i - i0, y0, tx0) + ch * 4]) = v;
+        }
+        continue;
+      }
 #pragma unroll
       for (int n = 0; n < kTR; ++n)
 #pragma unroll
@@ -219,7 +233,7 @@ __device__ __forceinline__ void pyramid_epilogue(const PyramidArgs& p, f32x16 (&
       }
     }
   }
-  if (p.nlev < 2) return;
+  if (p.nlev < 2 || (p.stagger_mode & 8)) return;  // (mode bit 3, experiment: level 0 alone)
 
   float v2[2][16];
   const int H1 = p.Hl[1], W1 = p.Wl[1];
@@ -273,7 +287,7 @@ __device__ __forceinline__ void pyramid_epilogue(const PyramidArgs& p, f32x16 (&
       const int ql = 4 * j + (lane >> 4);
       const int i = i0 + wave * 32 + ql;
       const float4 v = *reinterpret_cast<const float4*>(&sw[ql * 64 + ch * 4]);
-      if (i < p.N && (y1 >> 2) < p.HB[1] && (ch >> 3) < tb1)
+      if (i < p.N && (y1 >> 2) < p.HB[1] && (ch >> 3) < tb1 && !(p.stagger_mode & 64))
         *reinterpret_cast<float4*>(&lvl_base(p, 1, (size_t)b * Nn + i0)[lvl_off32(p, 1, i - i0, y1, tx0 >> 1) + ch * 4]) = v;
     }
     if (p.nlev < 3) return;
@@ -310,10 +324,10 @@ __device__ __forceinline__ void pyramid_epilogue(const PyramidArgs& p, f32x16 (&
       const int c = lane + 64 * it, ql = c >> 2, part = c & 3;
       const int i = i0 + wave * 32 + ql;
       const float4 v = *reinterpret_cast<const float4*>(&s2[ql * 16 + part * 4]);
-      if (i < p.N && (y2 >> 2) < p.HB[2] && (x2 >> 3) < p.WB[2])
+      if (i < p.N && (y2 >> 2) < p.HB[2] && (x2 >> 3) < p.WB[2] && !(p.stagger_mode & 64))
         *reinterpret_cast<float4*>(&lvl_base(p, 2, (size_t)b * Nn + i0)[lvl_off32(p, 2, i - i0, y2, x2) + part * 4]) = v;
     }
-    if (p.nlev >= 4 && lane < 32) {
+    if (p.nlev >= 4 && lane < 32 && !(p.stagger_mode & 96)) {
       const int y3 = ty0 >> 3, x3 = tx0 >> 3;
       const int i = i0 + wave * 32 + lane;
       const float4 v = *reinterpret_cast<const float4*>(&s2[512 + lane * 4]);
@@ -542,6 +556,8 @@ using namespace oflow;
 
 static int g_pyr_stagger_cycles = 0, g_pyr_stagger_mode = 1;
 // experiment hook (not part of include/oflow.h): delay part of the split pyramid's first workgroups by `cycles`
+// (mode & 3: which ones); ablations: mode & 4 no main loop, & 8 level 0 alone, & 16 level 0 stored unstaged, & 32 no
+// level-3 stores, & 64 no level 1-3 stores (pooled and staged all the same)
 extern "C" void oflow_exp_set_pyramid_stagger(int cycles, int mode) {
   g_pyr_stagger_cycles = cycles;
   g_pyr_stagger_mode = mode;
