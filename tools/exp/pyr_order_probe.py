@@ -1,6 +1,7 @@
 """A/B of the split pyramid's target-tile order (Sintel x8, C = 256): blocked 4x2 target tiles (default) vs row-major
 (oflow_exp_set_pyramid_stagger mode bit 7), full kernel and epilogue alone (bit 2), interleaved samples; levels
-compared bit for bit between the orders; plus the fp32 API pyramid (CorrBlock) at configs[1]. One JSON line."""
+compared bit for bit between the orders; plus the fp32 API pyramid (CorrBlock) at configs[1]. One JSON line.
+The blocked order (mode bit 7) was removed after this run (profiles/r05/s41_pyr_order.log)."""
 import ctypes
 import json
 import os
