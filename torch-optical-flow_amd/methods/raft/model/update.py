@@ -22,7 +22,15 @@ from optical_flow import _native
 
 
 # output-channel block (workgroup N) per update-block conv of the split path; tools/exp/run_conv_bn_ab.py A/Bs them
-CONV_BN = {"c2": 64, "f1": 128, "f2": 64, "mo": 128, "gru": 128, "fh1": 128}
+# output-channel block per update-block conv. r05 re-check on the graph bench (profiles/r05/s43-s45, alternated on one
+# box each): convc2 96 (two 96-channel blocks, each wave 32 px x 96 ch: 8 operand reads per 9 MFMA triples instead of
+# 6 per 6, the halo staged twice instead of three times) +2.0 %; with the flow head's first conv at 64 (register-direct
+# 64-channel blocks, 448 workgroups per lane) 444.2 / 444.8 / 444.8 vs 444.3 / 441.1 / 442.7 pairs/s for convc2 96
+# alone; the motion conv at 64 is +1.5 % alone but not on top of convc2 96, convf2 at 32 -2 %. Bit-identical (the
+# K order per output is the same for every block).
+CONV_BN = {"c2": 96, "f1": 128, "f2": 64, "mo": 128, "gru": 128, "fh1": 64}
+# (A/B runs: OFLOW_CONV_BN="c2=96,mo=64" overrides entries; any block the conv launcher accepts for that layer)
+CONV_BN.update({k: int(v) for k, v in (kv.split("=") for kv in os.environ.get("OFLOW_CONV_BN", "").split(",") if kv)})
 # the flow head's output conv (3x3, 256 -> 2) above the small-grid threshold: "conv" = the 3x3 conv with 2 of its 32
 # output columns used, coords1 += in its epilogue; "col2im" = a 1x1 conv 256 -> 18 (the 9 taps' products at the input
 # pixel, 18 of 32 MFMA columns used) + a gather of the 9 taps into coords1 (oflow_flow_head_col2im_f32). In-process A/B
