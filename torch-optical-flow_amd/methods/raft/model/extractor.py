@@ -9,6 +9,8 @@ stride-2 stages fed in space-to-depth layout. ``SmallEncoder``/``BottleneckBlock
 """
 from __future__ import annotations
 
+import os
+
 from typing import Optional, List, Sequence, Tuple, Union
 
 import torch
@@ -131,6 +133,10 @@ def _fold_bn(conv: nn.Conv2d, bn: nn.Module):
     return (w * alpha.view(-1, 1, 1, 1)).float(), (b * alpha + beta).float()
 
 
+# (A/B runs: OFLOW_ENC_BN="128=64,96=32" maps the encoder convs' default output-channel blocks to others)
+_ENC_BN_OVERRIDE = {int(k): int(v) for k, v in (kv.split("=") for kv in os.environ.get("OFLOW_ENC_BN", "").split(",") if kv)}
+
+
 class SplitEncoder:
     """Inference execution of a ``BasicEncoder`` (norm 'instance' or 'batch' in eval mode) on the split-fp16 kernels.
 
@@ -178,7 +184,8 @@ class SplitEncoder:
 
     @staticmethod
     def _bn(n: int) -> int:
-        return {64: 64, 96: 96, 128: 128}.get(n, 128 if n % 128 == 0 else 64 if n % 64 == 0 else 32)
+        bn = {64: 64, 96: 96, 128: 128}.get(n, 128 if n % 128 == 0 else 64 if n % 64 == 0 else 32)
+        return _ENC_BN_OVERRIDE.get(bn, bn)
 
     def _conv_norm(self, x, cw, shape, act, out=None, res=None, s2d=False, raw_only=False):
         """conv -> norm -> act [-> + res -> relu]: returns the S32 output (or (raw, alpha, beta) when raw_only)."""
