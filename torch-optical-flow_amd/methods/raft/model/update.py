@@ -27,10 +27,15 @@ from optical_flow import _native
 # 6 per 6, the halo staged twice instead of three times) +2.0 %; with the flow head's first conv at 64 (register-direct
 # 64-channel blocks, 448 workgroups per lane) 444.2 / 444.8 / 444.8 vs 444.3 / 441.1 / 442.7 pairs/s for convc2 96
 # alone; the motion conv at 64 is +1.5 % alone but not on top of convc2 96, convf2 at 32 -2 %. Bit-identical (the
-# K order per output is the same for every block).
+# K order per output is the same for every block). Those runs replay the graph, whose lanes run the flow branch inline
+# (model/graph.py); with the flow branch on a side stream beside convc1 -> convc2 (the eager forward) the same blocks
+# cost 1.2 % (eager 428.8 / 427.7 / 427.4 vs 432.2 / 434.7 / 432.4 pairs/s, s51), so that case keeps the r04 blocks
+# (CONV_BN_SIDE).
 CONV_BN = {"c2": 96, "f1": 128, "f2": 64, "mo": 128, "gru": 128, "fh1": 64}
-# (A/B runs: OFLOW_CONV_BN="c2=96,mo=64" overrides entries; any block the conv launcher accepts for that layer)
-CONV_BN.update({k: int(v) for k, v in (kv.split("=") for kv in os.environ.get("OFLOW_CONV_BN", "").split(",") if kv)})
+CONV_BN_SIDE = dict(CONV_BN, c2=64, fh1=128)
+# (A/B runs: OFLOW_CONV_BN="c2=96,mo=64" overrides entries of both; any block the conv launcher accepts for that layer)
+for _bn in (CONV_BN, CONV_BN_SIDE):
+    _bn.update({k: int(v) for k, v in (kv.split("=") for kv in os.environ.get("OFLOW_CONV_BN", "").split(",") if kv)})
 # the flow head's output conv (3x3, 256 -> 2) above the small-grid threshold: "conv" = the 3x3 conv with 2 of its 32
 # output columns used, coords1 += in its epilogue; "col2im" = a 1x1 conv 256 -> 18 (the 9 taps' products at the input
 # pixel, 18 of 32 MFMA columns used) + a gather of the 9 taps into coords1 (oflow_flow_head_col2im_f32). In-process A/B
@@ -420,30 +425,31 @@ class SplitUpdate:
         # group is read again only after the join).
         main = torch.cuda.current_stream(coords1.device)
         side = self.side_stream if self.streams else None
+        bns = CONV_BN_SIDE if side is not None else CONV_BN  # (channel blocks: see CONV_BN)
         f1_in = V(self.pm) if self.pm is not None else _native.FlowIn(coords1)
         if side is not None:
             side.wait_stream(main)
             with torch.cuda.stream(side):
                 _native.flow_prep(coords1, self.pm, (V(self.hx), 254), (V(self.rhx), 254))
-                conv(f1_in, w["f1"], CONV_BN["f1"], "relu", y0=V(self.f1))
-                conv(V(self.f1), w["f2"], CONV_BN["f2"], "relu", y0=V(self.cf, 6, 2))
+                conv(f1_in, w["f1"], bns["f1"], "relu", y0=V(self.f1))
+                conv(V(self.f1), w["f2"], bns["f2"], "relu", y0=V(self.cf, 6, 2))
             self._convc1(corr_in)
-            conv(V(self.c1), w["c2"], CONV_BN["c2"], "relu", y0=V(self.cf, 0, 6))
+            conv(V(self.c1), w["c2"], bns["c2"], "relu", y0=V(self.cf, 0, 6))
             main.wait_stream(side)
         else:
             _native.flow_prep(coords1, self.pm, (V(self.hx), 254), (V(self.rhx), 254))
             self._convc1(corr_in)
-            conv(V(self.c1), w["c2"], CONV_BN["c2"], "relu", y0=V(self.cf, 0, 6))
-            conv(f1_in, w["f1"], CONV_BN["f1"], "relu", y0=V(self.f1))
-            conv(V(self.f1), w["f2"], CONV_BN["f2"], "relu", y0=V(self.cf, 6, 2))
-        conv(V(self.cf), w["mo"], CONV_BN["mo"], "relu", y0=V(self.hx, 4, 4), y1=V(self.rhx, 4, 4))
+            conv(V(self.c1), w["c2"], bns["c2"], "relu", y0=V(self.cf, 0, 6))
+            conv(f1_in, w["f1"], bns["f1"], "relu", y0=V(self.f1))
+            conv(V(self.f1), w["f2"], bns["f2"], "relu", y0=V(self.cf, 6, 2))
+        conv(V(self.cf), w["mo"], bns["mo"], "relu", y0=V(self.hx, 4, 4), y1=V(self.rhx, 4, 4))
         for tag, gx in zip(("1", "2"), self.gx):
-            conv(V(self.hx), w["zr" + tag], CONV_BN["gru"], epilogue=1, y0=V(self.rhx, 0, 4), gru_h=self.hm, gru_z=self.z,
+            conv(V(self.hx), w["zr" + tag], bns["gru"], epilogue=1, y0=V(self.rhx, 0, 4), gru_h=self.hm, gru_z=self.z,
                  addend=gx[:, :256])
-            conv(V(self.rhx), w["q" + tag], CONV_BN["gru"], epilogue=2, y0=V(self.hx, 0, 4), gru_h=self.hm, gru_z=self.z,
+            conv(V(self.rhx), w["q" + tag], bns["gru"], epilogue=2, y0=V(self.hx, 0, 4), gru_h=self.hm, gru_z=self.z,
                  addend=gx[:, 256:])
         net = V(self.hx, 0, 4)
-        conv(net, w["fh1"], CONV_BN["fh1"], "relu", y0=V(self.fh))
+        conv(net, w["fh1"], bns["fh1"], "relu", y0=V(self.fh))
         if self.flow_head_fma and coords1.is_contiguous():
             _native.flow_head2(V(self.fh), *w["fh2_f32"], coords1)  # coords1 += conv2(.) (raft.py:133)
         elif self.flow_head_mode == "tiled" and coords1.is_contiguous():
