@@ -14,4 +14,4 @@ for path in sorted(glob.glob(os.path.join("gpurun_out", sys.argv[1] + "*.log")),
         print(name, "NO LINE:", text[-400:].replace("\n", " | "))
         continue
     print(name, d["value"], d["ms_per_step"], "inflight", d["config"].get("steps_in_flight"),
-          "lookup_us", round(d["roofline"].get("launch_us", 0) or 0, 1), "frac", d.get("roofline", {}).get("frac"))
+          "lookup_us", round(d.get("roofline", {}).get("launch_us", 0) or 0, 1), "frac", d.get("roofline", {}).get("frac"))
