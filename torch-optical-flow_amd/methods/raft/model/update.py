@@ -24,8 +24,8 @@ from optical_flow import _native
 # output-channel block (workgroup N) per update-block conv of the split path; tools/exp/run_conv_bn_ab.py A/Bs them
 # output-channel block per update-block conv. r05 re-check on the graph bench (profiles/r05/s43-s45, alternated on one
 # box each): convc2 96 (two 96-channel blocks, each wave 32 px x 96 ch: 8 operand reads per 9 MFMA triples instead of
-# 6 per 6, the halo staged twice instead of three times) +2.0 %; with the flow head's first conv at 64 (register-direct
-# 64-channel blocks, 448 workgroups per lane) 444.2 / 444.8 / 444.8 vs 444.3 / 441.1 / 442.7 pairs/s for convc2 96
+# 6 per 6, the halo staged twice instead of three times) +2.0 %; with the flow head's first conv at 64 (LDS-staged
+# 64-channel blocks, 880 workgroups per lane) 444.2 / 444.8 / 444.8 vs 444.3 / 441.1 / 442.7 pairs/s for convc2 96
 # alone; the motion conv at 64 is +1.5 % alone but not on top of convc2 96, convf2 at 32 -2 %. Bit-identical (the
 # K order per output is the same for every block). Those runs replay the graph, whose lanes run the flow branch inline
 # (model/graph.py); with the flow branch on a side stream beside convc1 -> convc2 (the eager forward) the same blocks
