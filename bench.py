@@ -29,6 +29,7 @@ timed region: they time its last replay. ``--eager`` times the eager forward ins
 from __future__ import annotations
 
 import argparse
+import ctypes
 import json
 import os
 import statistics
@@ -405,6 +406,14 @@ def main() -> int:
     from model import RAFT, InputPadder, synthetic
     from model.pair_sharding import infer_sharded, infer_sharded_pipelined
     from optical_flow import _native
+    # experiments only: OFLOW_EXP_CALLS="oflow_exp_set_bn64_8row=1;..." calls liboflow's int-argument experiment setters
+    for call in filter(None, os.environ.get("OFLOW_EXP_CALLS", "").split(";")):
+        name, val = call.split("=")
+        if not name.startswith("oflow_exp_set_"):
+            raise SystemExit(f"bench: OFLOW_EXP_CALLS takes oflow_exp_set_* setters, not {name}")
+        fn = getattr(_native.load(), name)
+        fn.argtypes, fn.restype = [ctypes.c_int], None
+        fn(int(val))
 
     ppg, h, w, iters, pmode, alt = WORKLOADS[args.workload]
     ppg = args.pairs_per_gpu or ppg

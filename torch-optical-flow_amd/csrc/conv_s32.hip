@@ -1082,11 +1082,12 @@ int launch_conv(const ConvArgs& a0, hipStream_t s) {
 // In-process A/B (tools/exp/run_small_grid_ab.py): batch 1 x 24 iterations 12.9 -> 8.8 ms; a pixel threshold keeps
 // the 4-pair lanes of the 8-pair step (28160 px) on the default tiles, where the small ones cost +1.5-3 %.
 int g_small_grid_px = 16384;  // output-pixel count under which the small tiles are used (0: never; experiments only)
-// instance-norm convs (encoders, BN 64) on 8-row tiles too (experiments only; outputs bit-identical). Alone the 8-row
-// tiles are 0-12 % faster per layer, but in the step, where fnet's halves and cnet share the chip, their 71 KB of LDS
-// per workgroup crowds the other streams' workgroups: interleaved in-process A/B 20.40 (4-row) vs 20.69-20.90 ms
-// (profiles/r03/exp/s8b_ab_enc.log).
-int g_stats_8row = 0;
+// instance-norm convs (encoders, BN 64) on 8-row tiles too (outputs bit-identical). Alone the 8-row tiles are 0-12 %
+// faster per layer; r03 measured the eager step slower with them (fnet's halves and cnet share the chip and their
+// 71 KB of LDS per workgroup crowded the other streams' workgroups: 20.40 (4-row) vs 20.69-20.90 ms,
+// profiles/r03/exp/s8b_ab_enc.log). r05, on the replayed graph with the r05 kernels: 457.5 / 457.4 vs 453.6 / 453.9
+// pairs/s (profiles/r05/s58_*.log), so on by default (oflow_exp_set_stats_8row(0) restores the 4-row tiles).
+int g_stats_8row = 1;
 int g_conv_exp_flags = 0;
 // BN 64 convs without instance-norm partials (cnet's layer1, convc2, the motion conv) on 8-row tiles (experiments
 // only). r02 adopted them from per-layer timings; in the step (concurrent streams) the 4-row tiles win: interleaved
