@@ -3,6 +3,11 @@
     python bench.py [--gpus N] [--steps K] [--warmup W] [--workload sintel|kitti|corr]
     torchrun --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 --master-port P bench.py --gpus N ...
 
+Both forms run N ranks. Under torchrun (WORLD_SIZE set) this process is one rank. Without WORLD_SIZE and with
+--gpus N > 1, this process is only a launcher (``launch_ranks``): before any GPU call it starts N fresh rank processes
+of this script (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_ADDR=127.0.0.1 / MASTER_PORT in their environment), waits
+for them, forwards rank 0's JSON line as its only stdout line and exits with the first non-zero rank exit code.
+
 Default workload "sintel" = BASELINE configs[3] per rank: every GPU infers 8 Sintel pairs (436x1024, padded
 440x1024 in predict.py's 'sintel' mode) per step, 12 GRU iterations, fp32, test_mode; the global batch is 8*N
 pairs (weak scaling; N = 8 is configs[3]'s 64 pairs). A step is: rank 0 scatters the pairs over RCCL (inputs
@@ -51,6 +56,7 @@ MFMA_F32_PEAK_TFLOPS = 157.3  # dense fp32 MFMA (v_mfma_f32_32x32x2_f32), spec
 MFMA_F16_PEAK_TFLOPS = 2500.0  # dense fp16 MFMA, spec (no sparsity)
 PMC_TRAFFIC_FILE = os.path.join(REPO, "profiles", "lookup_traffic.json")
 BATCH_GOLDEN = os.path.join(REPO, "tests", "golden", "raft_e2e_batch.npz")
+HD_GOLDEN = os.path.join(REPO, "tests", "golden", "raft_e2e_hd.npz")
 # the reference forward's FLOPs per pair (12 iterations, measured with the torch profiler)
 REF_GFLOP_PER_PAIR = {"sintel": 735.9, "kitti": 767.6}
 
@@ -288,13 +294,15 @@ def cpu_baseline(h: int, w: int, iters: int, pairs: int):
 
 def batch_golden(workload: str, h: int, w: int, iters: int):
     """(tag, fixture) of the reference-generated batch golden matching this workload's frame size and iterations, or
-    (None, None): 'sintel8' / 'kitti8' (tests/golden/gen_goldens.py BATCH_CASES: 8 pairs, 12 iterations)."""
+    (None, None): 'sintel8' / 'kitti8' (tests/golden/gen_goldens.py BATCH_CASES: 8 pairs, 12 iterations) and 'hd1'
+    (HD_CASES: one 1080x1920 pair, 12 iterations, the reference's dense fp32 CPU path)."""
     import numpy as np
 
-    tag = {"sintel": "sintel8", "kitti": "kitti8"}.get(workload)
-    if tag is None or not os.path.exists(BATCH_GOLDEN):
+    tag, path = {"sintel": ("sintel8", BATCH_GOLDEN), "kitti": ("kitti8", BATCH_GOLDEN),
+                 "hd": ("hd1", HD_GOLDEN)}.get(workload, (None, None))
+    if tag is None or not os.path.exists(path):
         return None, None
-    g = np.load(BATCH_GOLDEN, allow_pickle=False)
+    g = np.load(path, allow_pickle=False)
     b, gh, gw, giters, s, seed = (int(v) for v in g[f"{tag}_cfg"])
     if (gh, gw, giters) != (h, w, iters):
         return None, None
@@ -319,7 +327,8 @@ def step_epe(out, tag: str, g, n_pairs: int):
         "up_mean": float(eu.mean()),
         "up_max": float(eu.max()),
         "unit": "px",
-        "tolerance": "mean <= 1e-4, max <= 1e-3 px (SURVEY §8(c))",
+        "tolerance": ("mean <= 2e-3, max <= 2e-2 px (SURVEY §8(c), fp16 on-the-fly corr)" if tag == "hd1"
+                      else "mean <= 1e-4, max <= 1e-3 px (SURVEY §8(c))"),
     }
 
 
@@ -353,6 +362,100 @@ def golden_epe(model, dev, workload: str):
     }
 
 
+def _free_port() -> int:
+    import socket
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(n: int, argv) -> int:
+    """``--gpus N`` (N > 1) outside torchrun: start N rank processes of this script and wait for them.
+
+    The launcher itself never touches the GPU (it only imports torch, which initialises nothing) and never replaces
+    itself (no exec): every rank is a fresh child process with RANK = LOCAL_RANK = r, WORLD_SIZE = N and a free
+    MASTER_PORT on 127.0.0.1, and runs this script's rank path (one GPU each, RCCL). Rank 0's stdout JSON line is
+    forwarded as the launcher's only stdout line; every other output line goes to stderr. When a rank exits non-zero
+    the others are terminated (a peer blocked in a collective would otherwise wait forever) and the launcher returns
+    that first non-zero exit code."""
+    import subprocess
+    import threading
+
+    port = _free_port()
+    procs, threads = [], []
+    lock = threading.Lock()
+
+    def pump(stream, r):
+        for raw in iter(stream.readline, b""):
+            line = raw.decode(errors="replace")
+            json_line = False
+            if r == 0 and line.startswith("{"):
+                try:
+                    json_line = "metric" in json.loads(line)
+                except ValueError:
+                    pass
+            with lock:
+                (sys.stdout if json_line else sys.stderr).write(line if json_line else f"[rank {r}] {line}")
+                (sys.stdout if json_line else sys.stderr).flush()
+        stream.close()
+
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        p = subprocess.Popen([sys.executable, "-u", os.path.abspath(__file__), *argv], env=env,
+                             stdout=subprocess.PIPE, stderr=subprocess.STDOUT)
+        procs.append(p)
+        t = threading.Thread(target=pump, args=(p.stdout, r), daemon=True)
+        t.start()
+        threads.append(t)
+    first_bad = 0
+    try:
+        pending = set(range(n))
+        while pending:
+            for r in sorted(pending):
+                rc = procs[r].poll()
+                if rc is None:
+                    continue
+                pending.discard(r)
+                if rc != 0 and first_bad == 0:
+                    first_bad = rc if rc > 0 else 128 - rc
+                    print(f"bench: rank {r} exited with {rc}; stopping the other ranks", file=sys.stderr)
+                    for q in pending:
+                        procs[q].terminate()
+            time.sleep(0.05)
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+                p.wait()
+        for t in threads:
+            t.join(timeout=10)
+    return first_bad
+
+
+def _standin_rank(world: int, rank: int, fail_rank: int) -> int:
+    """Test stand-in for a rank (``--standin-worker``, CPU only): a gloo group over the launcher's rendezvous, one
+    all-reduce of (rank + 1), a per-rank line on stderr and rank 0's JSON line -- the launcher's plumbing without the
+    GPU (tests/test_bench_launcher.py). ``fail_rank`` exits 3 before the rendezvous, leaving its peers blocked in
+    it: the launcher must stop them and return 3."""
+    if rank == fail_rank:
+        print(f"standin rank {rank}: failing on purpose", file=sys.stderr, flush=True)
+        return 3
+    if world == 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", str(_free_port()))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    t = torch.tensor([rank + 1], dtype=torch.int64)
+    dist.all_reduce(t)
+    print(f"standin rank {rank} of {world}: sum {int(t.item())}", file=sys.stderr, flush=True)
+    if rank == 0:
+        print(f"not a json line from rank {rank}", flush=True)
+        print(json.dumps({"metric": METRIC, "n_gpus": world, "rank_sum": int(t.item())}), flush=True)
+    dist.destroy_process_group()
+    return 0
+
+
 def main() -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -383,7 +486,14 @@ def main() -> int:
                          "infer_sharded_pipelined)")
     ap.add_argument("--range-guard", default=None, choices=["sync", "deferred", "off"],
                     help="RAFT.range_guard (default: the model's, 'deferred': checked after the timed region)")
+    ap.add_argument("--standin-worker", action="store_true", help=argparse.SUPPRESS)
+    ap.add_argument("--standin-fail-rank", type=int, default=-1, help=argparse.SUPPRESS)
     args = ap.parse_args()
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        return launch_ranks(args.gpus, sys.argv[1:])  # this process is only the launcher: no GPU call before this
+    if args.standin_worker:
+        return _standin_rank(int(os.environ.get("WORLD_SIZE", "1")), int(os.environ.get("RANK", "0")),
+                             args.standin_fail_rank)
     if args.graph and args.eager:
         print("bench: --graph and --eager exclude each other", file=sys.stderr)
         return 2
@@ -446,7 +556,7 @@ def main() -> int:
                 out = cb(cgrid)
             return out, out
 
-    gtag, gfix = batch_golden(args.workload, h, w, iters) if args.workload != "corr" and not alt else (None, None)
+    gtag, gfix = batch_golden(args.workload, h, w, iters) if args.workload != "corr" else (None, None)
     if args.workload != "corr" and rank == 0:
         # the golden batch's pairs (8 distinct pairs for sintel / kitti), tiled to the global batch, in rank 0's HBM
         npairs = int(gfix[f"{gtag}_cfg"][0]) if gtag else 2
@@ -490,10 +600,8 @@ def main() -> int:
             graphed = graphs[gturn[0] % ngraphs]
             gturn[0] += 1
             low, up = graphed(p0, p1)
-            if world > 1:
-                # the graph's outputs are overwritten by the next replay, while this step's gathers may still be
-                # reading them on the communicator's stream (pipelined driver): hand them copies
-                return low.clone(), padder.unpad(up).clone()
+            # the graph's outputs are overwritten by the next replay; with N > 1 the pipelined driver's gathers send
+            # private copies (model/pair_sharding.py infer_sharded_pipelined), so these may be returned as they are
             return low, padder.unpad(up)
 
     def step():

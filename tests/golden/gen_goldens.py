@@ -10,7 +10,7 @@ written. Bytecode writing is disabled so the read-only tree stays untouched.
 Inputs come from the repository's own deterministic generators (``model/synthetic.py``), which the GPU box
 re-runs bit-for-bit; fmaps are therefore not stored, only a float64 checksum that the tests re-verify.
 
-Usage:  python tests/golden/gen_goldens.py [corr] [warp] [raft] [batch] [io]   (default: all)
+Usage:  python tests/golden/gen_goldens.py [corr] [warp] [raft] [batch] [io] [hd]   (default: all)
 """
 from __future__ import annotations
 
@@ -216,6 +216,41 @@ def gen_raft_batch(RAFT, InputPadder) -> None:
     np.savez_compressed(os.path.join(HERE, "raft_e2e_batch.npz"), **out)
 
 
+HD_CASES = {
+    # BASELINE configs[4]: one 1080x1920 pair, 12 iterations, 'sintel' padding (1088x1920). The reference's alternate
+    # corr needs its alt_cuda_corr CUDA extension (absent, and not runnable on CPU), so the golden is the reference's
+    # dense fp32 CPU path: the same correlation values (corr.py:38-87 vs the AlternateCorrBlock's definition); the GPU
+    # test runs RAFT(alternate_corr=True) against it at SURVEY §8(c)'s fp16 bar.
+    "hd1": dict(B=1, H=1080, W=1920, iters=12, stride=8, mode="sintel", seed=11),
+}
+
+
+def gen_raft_hd(RAFT, InputPadder) -> None:
+    """RAFT forward(test_mode=True) at 1080p (`raft.py:87-147`), written to raft_e2e_hd.npz in raft_e2e_batch.npz's
+    layout: the full 1/8-res flow, the full-res flow at stride 8, input checksums."""
+    torch.set_num_threads(max(1, os.cpu_count() or 1))
+    model = RAFT()
+    model.load_state_dict(synthetic.synthetic_state_dict(model.state_dict()))
+    model.eval()
+    out = {}
+    with torch.inference_mode():
+        for tag, c in HD_CASES.items():
+            img0, img1 = synthetic.synthetic_pair(c["B"], c["H"], c["W"], seed=c["seed"])
+            padder = InputPadder(img0.shape, mode=c["mode"])
+            p0, p1 = padder.pad(img0, img1)
+            low, up = model(p0, p1, iters=c["iters"], test_mode=True)
+            up = padder.unpad(up)
+            s = c["stride"]
+            out[f"{tag}_cfg"] = np.array([c["B"], c["H"], c["W"], c["iters"], s, c["seed"]], dtype=np.int64)
+            out[f"{tag}_mode"] = np.array(c["mode"])
+            out[f"{tag}_low"] = low.numpy()
+            out[f"{tag}_up"] = up[..., ::s, ::s].contiguous().numpy()
+            out[f"{tag}_up_checksum"] = _checksum(up)
+            out[f"{tag}_img_checksum"] = np.stack([_checksum(img0), _checksum(img1)])
+            print(tag, "flow_up mean |f| =", float(up.norm(dim=1).mean()), flush=True)
+    np.savez_compressed(os.path.join(HERE, "raft_e2e_hd.npz"), **out)
+
+
 def io_flows():
     """Flow fields of the I/O goldens, from the repository's own generators (the tests rebuild them)."""
     flows = {
@@ -279,7 +314,7 @@ def main() -> int:
         print("gen_goldens: /root/reference absent; fixtures are committed, nothing to do")
         return 0
     RAFT, CorrBlock, InputPadder, bilinear_sampler, coords_grid, ref_operator = _import_reference()
-    which = sys.argv[1:] or ["corr", "warp", "raft", "batch", "io"]
+    which = sys.argv[1:] or ["corr", "warp", "raft", "batch", "io", "hd"]
     if "corr" in which:
         gen_corr(CorrBlock, coords_grid)
     if "warp" in which:
@@ -290,6 +325,8 @@ def main() -> int:
         gen_raft_batch(RAFT, InputPadder)
     if "io" in which:
         gen_io()
+    if "hd" in which:
+        gen_raft_hd(RAFT, InputPadder)
     return 0
 
 

@@ -81,3 +81,27 @@ def test_raft_alternate_corr_matches_reference_flow(golden):
         e = torch.norm(up - torch.from_numpy(g[f"{tag}_up"]), dim=1)
         print(f"{tag} alternate_corr fp16: EPE mean {float(e.mean()):.2e} max {float(e.max()):.2e}")
         assert float(e.mean()) <= 2e-3 and float(e.max()) <= 2e-2
+
+
+def test_raft_alternate_corr_matches_reference_flow_at_1080p(golden):
+    """configs[4] end to end at its own resolution: RAFT(alternate_corr=True) on the on-the-fly fp16 corr kernels,
+    one 1080x1920 pair ('sintel' padding to 1088x1920, 135 x 240 queries), 12 iterations, against the reference's
+    flows for the same pair (tests/golden/raft_e2e_hd.npz: its dense fp32 CPU path -- the reference's alternate corr
+    needs a CUDA extension). SURVEY §8(c) fp16 bar: mean EPE <= 2e-3 px, max <= 2e-2 px, on the 1/8-res flow and on
+    the full-res flow at stride 8."""
+    g = golden("raft_e2e_hd")
+    b, h, w, iters, s, seed = (int(v) for v in g["hd1_cfg"])
+    img0, img1 = synthetic.synthetic_pair(b, h, w, seed=seed)
+    padder = InputPadder(img0.shape, mode=str(g["hd1_mode"]))
+    model = RAFT(alternate_corr=True).eval()
+    model.load_state_dict(synthetic.synthetic_state_dict(model.state_dict()))
+    model = model.to(DEV)
+    with torch.inference_mode():
+        low, up = model(*(x.to(DEV) for x in padder.pad(img0, img1)), iters=iters, test_mode=True)
+    up = padder.unpad(up)[..., ::s, ::s].cpu()
+    el = torch.norm(low.float().cpu() - torch.from_numpy(g["hd1_low"]), dim=1)
+    eu = torch.norm(up - torch.from_numpy(g["hd1_up"]), dim=1)
+    print(f"1080p alternate_corr fp16: EPE low mean {float(el.mean()):.2e} max {float(el.max()):.2e}, "
+          f"up mean {float(eu.mean()):.2e} max {float(eu.max()):.2e}")
+    assert float(el.mean()) <= 2e-3 and float(el.max()) <= 2e-2
+    assert float(eu.mean()) <= 2e-3 and float(eu.max()) <= 2e-2

@@ -138,7 +138,9 @@ def test_bench_batch_golden_and_step_epe(golden):
         e = bench.step_epe((low, up), t, g, 8)
         assert e["pairs"] == 8 and e["low_max"] == 0.0 and e["up_max"] == 0.0
     assert bench.batch_golden("sintel", 436, 1024, 24) == (None, None)  # other iteration counts: no batch golden
-    assert bench.batch_golden("hd", 1080, 1920, 12) == (None, None)
+    t, g = bench.batch_golden("hd", 1080, 1920, 12)  # configs[4]: the reference's 1080p pair
+    assert t == "hd1" and tuple(int(v) for v in g["hd1_cfg"][:4]) == (1, 1080, 1920, 12)
+    assert bench.batch_golden("hd", 1080, 1920, 24) == (None, None)
 
 
 def test_cached_pack_keys_and_rebuilds():

@@ -147,3 +147,25 @@ def test_batch_golden_input_checksums(golden):
         img0, img1 = synthetic.synthetic_pair(b, h, w, seed=seed)
         chk = np.stack([[float(x.double().sum()), float((x.double() ** 2).sum()), float(x.abs().max())] for x in (img0, img1)])
         assert np.array_equal(chk, g[f"{tag}_img_checksum"]), tag
+
+
+def test_hd_golden_inputs_and_oracle(golden):
+    """raft_e2e_hd.npz (BASELINE configs[4]: one 1080x1920 pair, 12 iterations, made by the reference's dense fp32
+    CPU path): the frames are the repository's generator output (input checksums), and the oracle's forward of the
+    pair matches the reference's flows at the fp32 bar -- the oracle is pinned at the configs[4] size too."""
+    g = golden("raft_e2e_hd")
+    b, h, w, iters, s, seed = (int(v) for v in g["hd1_cfg"])
+    assert (b, h, w, iters) == (1, 1080, 1920, 12)
+    img0, img1 = synthetic.synthetic_pair(b, h, w, seed=seed)
+    chk = np.stack([[float(x.double().sum()), float((x.double() ** 2).sum()), float(x.abs().max())] for x in (img0, img1)])
+    assert np.array_equal(chk, g["hd1_img_checksum"])
+    model = oraft.RAFT().eval()
+    model.load_state_dict(synthetic.synthetic_state_dict(model.state_dict()))
+    padder = oraft.InputPadder(img0.shape, mode=str(g["hd1_mode"]))
+    with torch.inference_mode():
+        low, up = model(*padder.pad(img0, img1), iters=iters, test_mode=True)
+    up = padder.unpad(up)[..., ::s, ::s]
+    epe_low = oraft.end_point_error(low, torch.from_numpy(g["hd1_low"]))
+    epe_up = oraft.end_point_error(up, torch.from_numpy(g["hd1_up"]))
+    assert float(epe_low.mean()) <= 1e-4 and float(epe_low.max()) <= 1e-3
+    assert float(epe_up.mean()) <= 1e-4 and float(epe_up.max()) <= 1e-3

@@ -163,9 +163,10 @@ def test_scatter_refuses_a_shape_that_disagrees_with_the_batch(world):
         assert r[1] == ("ValueError", "ok", "nan", "none"), r
 
 
-def _pipeline_worker(rank, world, port, batch, steps, q):
+def _pipeline_worker(rank, world, port, batch, steps, reuse, q):
     """infer_sharded_pipelined (scatter of step i+1 and gathers of step i in flight around step i's forward) vs
-    infer_sharded step by step, on distinct batches per step."""
+    infer_sharded step by step, on distinct batches per step. ``reuse``: the forward returns the same two output
+    buffers every call, overwritten in place (as GraphedRAFT's replayed outputs are)."""
     from model.pair_sharding import infer_sharded_pipelined
 
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
@@ -180,10 +181,18 @@ def _pipeline_worker(rank, world, port, batch, steps, q):
         seq = [infer_sharded(_fake_forward, *(d if rank == 0 else (None, None)), cpu, shape=shape, flow_shapes=flow_shapes)
                for d in data]
         calls = []
+        bufs = {}
 
         def fwd(a, b):
             calls.append(a.shape[0])
-            return _fake_forward(a, b)
+            lo, up = _fake_forward(a, b)
+            if not reuse:
+                return lo, up
+            if not bufs:
+                bufs["lo"], bufs["up"] = torch.empty_like(lo), torch.empty_like(up)
+            bufs["lo"].copy_(lo)
+            bufs["up"].copy_(up)
+            return bufs["lo"], bufs["up"]
 
         batches = (d if rank == 0 else (None, None) for d in data)
         pipe = list(infer_sharded_pipelined(fwd, batches, cpu, shape=shape, flow_shapes=flow_shapes))
@@ -200,9 +209,11 @@ def _pipeline_worker(rank, world, port, batch, steps, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,batch,steps", [(2, 8, 3), (2, 5, 1), (3, 2, 2)])
-def test_pipelined_steps_equal_sequential_gloo(world, batch, steps):
+@pytest.mark.parametrize("world,batch,steps,reuse", [(2, 8, 3, False), (2, 5, 1, False), (3, 2, 2, False),
+                                                     (2, 8, 4, True), (3, 7, 3, True)])
+def test_pipelined_steps_equal_sequential_gloo(world, batch, steps, reuse):
     """The overlapped step driver bench.py --gpus N uses returns every step's flows exactly as the sequential
-    scatter -> forward -> gather does, including a ragged batch, one step, and a rank without pairs."""
-    res = _run(_pipeline_worker, world, batch, steps)
+    scatter -> forward -> gather does, including a ragged batch, one step, a rank without pairs, and a forward that
+    overwrites one pair of output buffers per call (the gathers still in flight send private copies)."""
+    res = _run(_pipeline_worker, world, batch, steps, reuse)
     assert all(r[1] for r in res), res

@@ -135,10 +135,11 @@ class _PendingGather:
     """An issued (async) gather of flow shards to ``dst``: ``result()`` waits for it and returns the (B, ...) batch on
     ``dst``, None elsewhere."""
 
-    __slots__ = ("work", "gather_list", "global_batch", "world", "is_dst")
+    __slots__ = ("work", "send", "gather_list", "global_batch", "world", "is_dst")
 
-    def __init__(self, work, gather_list, global_batch: int, world: int, is_dst: bool) -> None:
-        self.work, self.gather_list, self.global_batch, self.world, self.is_dst = work, gather_list, global_batch, world, is_dst
+    def __init__(self, work, send, gather_list, global_batch: int, world: int, is_dst: bool) -> None:
+        self.work, self.send, self.gather_list = work, send, gather_list
+        self.global_batch, self.world, self.is_dst = global_batch, world, is_dst
 
     def result(self) -> Optional[Tensor]:
         if self.work is not None:
@@ -152,17 +153,21 @@ class _PendingGather:
         return torch.cat(parts, dim=0)
 
 
-def _gather(flow: Tensor, global_batch: int, dst: int, group, async_op: bool) -> _PendingGather:
+def _gather(flow: Tensor, global_batch: int, dst: int, group, async_op: bool, own: bool = False) -> _PendingGather:
+    """Issue the gather of ``flow`` (padded to the common chunk). ``own``: send a private copy even when ``flow`` is
+    already a contiguous chunk, so that the caller may overwrite ``flow`` (a graph replay's output buffer, a reused
+    workspace) while the gather is still reading on the communicator's stream; the copy is made on the current stream
+    before the collective is issued, so it is ordered before the send."""
     world, rank = _world(group)
     chunk = -(-global_batch // world)
     rest = list(flow.shape[1:])
-    send = flow
     if flow.shape[0] < chunk:
         send = torch.cat([flow, flow.new_zeros([chunk - flow.shape[0]] + rest)], dim=0)
-    send = send.contiguous()
+    else:
+        send = flow.clone(memory_format=torch.contiguous_format) if own else flow.contiguous()
     gather_list = [torch.empty_like(send) for _ in range(world)] if rank == dst else None
     w = dist.gather(send, gather_list, dst=_src_rank(group, dst), group=group, async_op=async_op)
-    return _PendingGather(w, gather_list, global_batch, world, rank == dst)
+    return _PendingGather(w, send, gather_list, global_batch, world, rank == dst)
 
 
 def gather_flows(flow: Tensor, global_batch: int, dst: int = 0, group=None) -> Optional[Tensor]:
@@ -224,7 +229,11 @@ def infer_sharded_pipelined(
     Yields each step's (flow_low, flow_up) on ``src`` ((None, None) elsewhere) one step late, then the last one: the
     same flows, in the same order, as ``infer_sharded`` per step (tests/test_sharding_gloo.py). Collectives are issued
     in the same order on every rank: scatter 0, then per step i: scatter i+1, gathers i. Shapes are fixed for the run
-    (``shape`` global (B, C, H, W), ``flow_shapes`` as in ``infer_sharded``)."""
+    (``shape`` global (B, C, H, W), ``flow_shapes`` as in ``infer_sharded``).
+
+    ``forward`` may return buffers it reuses on the next call (``GraphedRAFT``'s outputs are the graph's own and are
+    overwritten by every replay): step i's gathers send private copies made on the compute stream before they are
+    issued, so forward(i+1) cannot overwrite what the still-running gathers of step i read."""
     b = int(shape[0])
     it = iter(batches)
 
@@ -247,7 +256,8 @@ def infer_sharded_pipelined(
             up = s0.new_zeros([0] + list(flow_shapes[1]))
         else:
             low, up = forward(s0, s1)
-        gathers = (_gather(low, b, src, group, async_op=True), _gather(up, b, src, group, async_op=True), err)
+        gathers = (_gather(low, b, src, group, async_op=True, own=True),
+                   _gather(up, b, src, group, async_op=True, own=True), err)
         if prev is not None:
             out = prev[0].result(), prev[1].result()
             if prev[2] is not None:
