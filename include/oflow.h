@@ -174,7 +174,8 @@ int oflow_gru_blend_f32(const float* d_zr, long long szr, const float* d_bz, con
  *   epilogue 1 (GRU gates, N = 2*CH): n < CH -> z = sigmoid(.) into d_gru_z ([P][CH] fp32);
  *               n >= CH -> sigmoid(.) * d_gru_h[p][n-CH] into S32 d_y0 channel n-CH   (update.py:91-96)
  *   epilogue 2 (GRU candidate, N = CH): h = (1 - z) * h + z * tanh(.), in place in d_gru_h and into S32 d_y0
- *               (update.py:96-97). (act is ignored by epilogues 1 and 2.)
+ *               (update.py:96-97). (act is ignored by epilogues 1 and 2.) Epilogues 1 and 2 read / write d_gru_h
+ *               and d_gru_z as 16-B vectors: both must be 16-byte aligned (else OFLOW_E_ALIGN).
  * oflow_pack_s32_f32: d_x (B, C, H, W) fp32 with batch stride x_batch_stride -> act -> S32 d_y0 (and d_y1) channels
  *   dst_channel + c (dst_channel % 8 == 0; the last 8-channel chunk is zero-filled past C), and optionally a
  *   [P][nhwc_pixel_stride] fp32 copy.                                     (raft.py:115-118: tanh / relu of cnet)

@@ -53,7 +53,8 @@ def test_raft_matches_reference_flows(golden, tag, impl):
 @pytest.mark.parametrize("tag", ["sintel8", "kitti8"])
 def test_raft_matches_reference_flows_at_benchmarked_batch(golden, tag):
     """The forward bench.py times (8 pairs per GPU, 12 iterations, 'sintel' padding, default model: split encoders,
-    split-fp16 pyramid, lookup fused into convc1, two pair lanes, the flow head's output conv on the split MFMA kernel)
+    split-fp16 pyramid, lookup fused into convc1, two pair lanes, the flow head's output conv on the tiled fp32-FMA
+    kernel oflow_flow_head2_tiled_s32, FLOW_HEAD_MODE "tiled")
     against the reference's own flows for the same 8 pairs (tests/golden/raft_e2e_batch.npz), every pair."""
     from optical_flow import _native
 

@@ -1198,6 +1198,8 @@ int build_conv_args(ConvArgs& a, const void* d_x, long long x_pixel_stride, int 
   if ((x_pixel_stride & 15) || ((uintptr_t)d_x & 15) || ((uintptr_t)d_wpack & 15)) return OFLOW_E_ALIGN;
   if (epilogue == 0 && !d_y0 && !d_f32 && !d_nhwc && !d_stats) return OFLOW_E_NULL;
   if (epilogue != 0 && (!d_y0 || !d_gru_h || !d_gru_z || gru_channels <= 0 || gru_channels % 8)) return OFLOW_E_NULL;
+  // the GRU epilogues read h / z and write z as 16-B vectors (rows of gru_channels floats, n % 8 == 0)
+  if (epilogue != 0 && (((uintptr_t)d_gru_h & 15) || ((uintptr_t)d_gru_z & 15))) return OFLOW_E_ALIGN;
   if (epilogue == 1 && N != 2 * gru_channels) return OFLOW_E_SHAPE;
   if (epilogue == 2 && N != gru_channels) return OFLOW_E_SHAPE;
   if (epilogue != 0 && (d_nhwc || d_stats || d_res || s2d)) return OFLOW_E_MODE;

@@ -19,6 +19,8 @@ from torch import Tensor
 
 from optical_flow import _native
 
+from .update import CONV_BLOCKS, parse_block_overrides
+
 
 def _norm_layer(norm_fn: str, planes: int, groups: int) -> nn.Module:
     if norm_fn == "group":
@@ -134,7 +136,8 @@ def _fold_bn(conv: nn.Conv2d, bn: nn.Module):
 
 
 # (A/B runs: OFLOW_ENC_BN="128=64,96=32" maps the encoder convs' default output-channel blocks to others)
-_ENC_BN_OVERRIDE = {int(k): int(v) for k, v in (kv.split("=") for kv in os.environ.get("OFLOW_ENC_BN", "").split(",") if kv)}
+_ENC_BN_OVERRIDE = {int(k): v for k, v in
+                    parse_block_overrides("OFLOW_ENC_BN", {str(b) for b in CONV_BLOCKS}).items()}
 
 
 class SplitEncoder:

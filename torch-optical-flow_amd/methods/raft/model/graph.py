@@ -78,17 +78,19 @@ class GraphedRAFT:
             # stream, model/update.py _side_stream) are the ones the warm-up created
             # capture_active(): the pair lanes' streams join the capture through event waits and on ROCm do not report
             # themselves as capturing; the weight caches must not wait on their (pre-capture) events from any of them
-            _update._CAPTURE_DEPTH[0] += 1
             prev = _native._recorder
             if self.recorder is not None:
                 _native.set_event_recorder(self.recorder)
             try:
-                with torch.cuda.graph(self.graph, stream=side):
+                with _update.capturing(dev), torch.cuda.graph(self.graph, stream=side):
                     self.flow_low, self.flow_up = model(self.image0, self.image1, iters=iters, test_mode=True)
             finally:
-                _update._CAPTURE_DEPTH[0] -= 1
                 if self.recorder is not None:
                     _native.set_event_recorder(prev)
+            # the graph's event-record nodes point at these hipEvents: hold our own references, so that clearing or
+            # replacing the caller's recorder dict cannot destroy an event a later replay still records into
+            self._timing_events = [ev for k, v in (self.recorder or {}).items() if isinstance(v, list)
+                                   for pair in v for ev in pair]
 
     def __call__(self, image0: Tensor, image1: Tensor) -> Tuple[Tensor, Tensor]:
         if image0.shape != self.image0.shape or image1.shape != self.image1.shape:

@@ -273,7 +273,7 @@ class RAFT(nn.Module):
         forward; "deferred" (default) does not wait -- this forward's status is ``last_range_snapshot``
         (``.overflowed()`` waits for it), and a later forward or ``check_range()`` raises for it."""
         guard = self.range_guard in ("sync", "deferred") and image0.is_cuda and not torch.is_grad_enabled()
-        capturing = image0.is_cuda and capture_active()
+        capturing = image0.is_cuda and capture_active(image0.device)
         if guard and not capturing:
             self._range_before(image0.device)
         out = self._forward(image0, image1, iters, flow_init, test_mode)

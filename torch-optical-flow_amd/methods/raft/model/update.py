@@ -9,7 +9,9 @@ is not provided.
 """
 from __future__ import annotations
 
+import contextlib
 import os
+import threading
 from typing import Optional, Tuple
 
 import torch
@@ -33,9 +35,37 @@ from optical_flow import _native
 # (CONV_BN_SIDE).
 CONV_BN = {"c2": 96, "f1": 128, "f2": 64, "mo": 128, "gru": 128, "fh1": 64}
 CONV_BN_SIDE = dict(CONV_BN, c2=64, fh1=128)
-# (A/B runs: OFLOW_CONV_BN="c2=96,mo=64" overrides entries of both; any block the conv launcher accepts for that layer)
+CONV_BLOCKS = (32, 64, 96, 128)  # output-channel blocks conv_s32 instantiates
+
+
+def parse_block_overrides(var: str, keys) -> dict:
+    """An A/B override "k1=v1,k2=v2" from environment variable ``var``, validated at import: every key one of ``keys``,
+    every value a conv block of ``CONV_BLOCKS``; anything else raises ValueError naming the variable."""
+    spec = os.environ.get(var, "")
+    out = {}
+    for kv in filter(None, (s.strip() for s in spec.split(","))):
+        k, sep, v = kv.partition("=")
+        if not sep or not v.strip().isdigit():
+            raise ValueError(f"{var}={spec!r}: expected comma-separated key=block entries, got {kv!r}")
+        key = k.strip()
+        if keys is not None and key not in keys:
+            raise ValueError(f"{var}={spec!r}: unknown key {key!r} (one of {sorted(keys)})")
+        if int(v) not in CONV_BLOCKS:
+            raise ValueError(f"{var}={spec!r}: block {v} for {key!r} is not one of {CONV_BLOCKS}")
+        out[key] = int(v)
+    return out
+
+
+def _env_choice(var: str, default: str, choices) -> str:
+    v = os.environ.get(var, default)
+    if v not in choices:
+        raise ValueError(f"{var}={v!r}: expected one of {list(choices)}")
+    return v
+
+
+# (A/B runs only: OFLOW_CONV_BN="c2=96,mo=64" overrides entries of both)
 for _bn in (CONV_BN, CONV_BN_SIDE):
-    _bn.update({k: int(v) for k, v in (kv.split("=") for kv in os.environ.get("OFLOW_CONV_BN", "").split(",") if kv)})
+    _bn.update(parse_block_overrides("OFLOW_CONV_BN", set(CONV_BN)))
 # the flow head's output conv (3x3, 256 -> 2) above the small-grid threshold: "conv" = the 3x3 conv with 2 of its 32
 # output columns used, coords1 += in its epilogue; "col2im" = a 1x1 conv 256 -> 18 (the 9 taps' products at the input
 # pixel, 18 of 32 MFMA columns used) + a gather of the 9 taps into coords1 (oflow_flow_head_col2im_f32). In-process A/B
@@ -44,11 +74,11 @@ for _bn in (CONV_BN, CONV_BN_SIDE):
 # r05: "tiled" = oflow_flow_head2_tiled_s32 (fp32 FMAs on an LDS-staged halo, 512 threads per 4 x 32 tile): step A/B
 # 18.81 vs 18.89 ms against "conv" (profiles/r05/s33_flow_head_tiled_ab.log; the first 256-thread form was 0.25 ms
 # slower, s32): the default; two channel groups per staging pass: +0.6 % on the graph bench (s37), bit-identical
-FLOW_HEAD_MODE = os.environ.get("OFLOW_FLOW_HEAD_MODE", "tiled")
+FLOW_HEAD_MODE = _env_choice("OFLOW_FLOW_HEAD_MODE", "tiled", ("tiled", "conv", "col2im"))
 # convf1 (7x7, 2 -> 128) straight from coords1 (_native.FlowIn, OFLOW_IN_FLOW7: each tile stages its flow window and
 # builds the patch operand in LDS) from this many pixels of the whole forward's batch up; below it flow_prep writes the
 # patch matrix and convf1 runs on the small-grid tiles. Bit-identical either way (same patch values, same k order).
-CONVF1_FROM_FLOW_MIN_PIXELS = 16384 if os.environ.get("OFLOW_CONVF1_FROM_FLOW", "1") != "0" else 1 << 62  # (0: A/B)
+CONVF1_FROM_FLOW_MIN_PIXELS = 16384 if _env_choice("OFLOW_CONVF1_FROM_FLOW", "1", ("0", "1")) == "1" else 1 << 62  # (0: A/B)
 
 class FlowHead(nn.Module):
     def __init__(self, input_dim: int = 128, hidden_dim: int = 256) -> None:
@@ -215,15 +245,32 @@ def _side_stream(device: torch.device, slot: int = 0) -> "torch.cuda.Stream":
     return _SIDE_STREAMS[key]
 
 
-_CAPTURE_DEPTH = [0]  # > 0 while GraphedRAFT captures a forward (model/graph.py)
+_CAPTURE = threading.local()  # per thread: {device index: depth} while GraphedRAFT captures a forward (model/graph.py)
 
 
-def capture_active() -> bool:
-    """Whether a HIP graph capture of a forward is in progress. Not ``torch.cuda.is_current_stream_capturing()`` alone:
-    a pair lane's stream joins the capture through an event wait, and on ROCm such a stream does not report itself as
-    capturing, so a check on it alone let the lane wait on an event recorded before the capture -- a dependency the
-    captured graph cannot hold (the two-lane capture crashed in capture_end: profiles/r04/s12_graph8.log)."""
-    return _CAPTURE_DEPTH[0] > 0 or torch.cuda.is_current_stream_capturing()
+@contextlib.contextmanager
+def capturing(device: torch.device):
+    """Marks a GraphedRAFT capture of a forward on ``device`` in progress on this thread (see ``capture_active``)."""
+    depth = _CAPTURE.__dict__.setdefault("depth", {})
+    idx = torch.device(device).index
+    depth[idx] = depth.get(idx, 0) + 1
+    try:
+        yield
+    finally:
+        depth[idx] -= 1
+
+
+def capture_active(device: Optional[torch.device] = None) -> bool:
+    """Whether a HIP graph capture of a forward on ``device`` (default: the current device) is in progress on this
+    thread. Not ``torch.cuda.is_current_stream_capturing()`` alone: a pair lane's stream joins the capture through an
+    event wait, and on ROCm such a stream does not report itself as capturing, so a check on it alone let the lane wait
+    on an event recorded before the capture -- a dependency the captured graph cannot hold (the two-lane capture crashed
+    in capture_end: profiles/r04/s12_graph8.log). Keyed by thread and device: a forward on another thread or device
+    while one is captured keeps its weight-cache waits and its range guard."""
+    idx = torch.device(device).index if device is not None else torch.cuda.current_device()
+    if _CAPTURE.__dict__.get("depth", {}).get(idx, 0) > 0:
+        return True
+    return torch.cuda.is_current_stream_capturing()
 
 
 def _module_device(module: nn.Module) -> Optional[torch.device]:
@@ -243,7 +290,7 @@ def cached_pack(module: nn.Module, key, build):
     if cache is not None and cache[0] == key:
         # (not while a graph is being captured: the capture must not depend on an event recorded outside it; a
         # capture follows warm-up forwards and a device sync, so the weights are complete)
-        if cache[2] is not None and on_gpu and not capture_active():
+        if cache[2] is not None and on_gpu and not capture_active(dev):
             torch.cuda.current_stream(dev).wait_event(cache[2])
         return cache[1]
     if on_gpu:

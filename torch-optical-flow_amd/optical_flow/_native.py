@@ -649,11 +649,11 @@ CHECK_RANGE = os.environ.get("OFLOW_CHECK", "0") not in ("", "0")
 F16_MAX = 65504.0
 # conv_s32 passes the fragment-major weights (ConvWeights.frag) to the 128-channel multi-tap convolutions: their B
 # operand goes to registers straight from HBM / L2 instead of through LDS (csrc/conv_s32.hip, BREG). Bit-identical.
-CONV_BREG = os.environ.get("OFLOW_CONV_BREG", "1") not in ("", "0")
-# ... and to the 64-channel 3x3 blocks (2 x 2 waves, each two row tiles x one 32-channel tile)
-CONV_BREG64 = os.environ.get("OFLOW_CONV_BREG64", "0") not in ("", "0")
-# ... and to the 32-channel 3x3 blocks (the flow head's output conv; 4 x 1 waves sharing the B fragments)
-CONV_BREG32 = os.environ.get("OFLOW_CONV_BREG32", "0") not in ("", "0")
+CONV_BREG = True
+# ... and (off: measured not faster; the tests exercise both) to the 64-channel 3x3 blocks
+# (2 x 2 waves, each two row tiles x one 32-channel tile) and to the 32-channel 3x3 blocks (4 x 1 waves)
+CONV_BREG64 = False
+CONV_BREG32 = False
 
 
 def _range_check(x, what: str) -> None:
