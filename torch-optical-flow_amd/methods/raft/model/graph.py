@@ -23,9 +23,11 @@ from . import update as _update
 
 # A multi-pair forward is captured with its pair lanes (RAFT.pair_lanes) but without the per-lane side streams of the
 # update block (update_block.split_streams): a side stream forked from a lane stream -- itself forked from the capture
-# stream -- makes hipStreamEndCapture segfault (profiles/r04/s12_graph8.log, profiles/r05/s1_probe_flag.log; the same
-# capture without those nested forks replays bit-identically, 18.57 ms vs 18.91 ms eager for 8 Sintel pairs:
-# profiles/r05/s2_probe_noside.log). The model's settings are restored after the capture. None: capture as configured.
+# stream -- makes hipStreamEndCapture segfault inside the HIP runtime PyTorch bundles (torch/lib/libamdhip64.so, 7.0.x):
+# the HIP-only reduction tools/exp/capture_fork_repro.hip crashes the same way on that runtime and captures correctly on
+# ROCm 7.2's (profiles/r06/r6s10_*, r6s11_*). The same capture without those nested forks replays
+# bit-identically, 18.57 ms vs 18.91 ms eager for 8 Sintel pairs (profiles/r05/s2_probe_noside.log). The model's
+# settings are restored after the capture. None: capture as configured.
 CAPTURE_LANE_SIDE_STREAMS = False
 
 class GraphedRAFT:
