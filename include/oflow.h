@@ -347,6 +347,30 @@ int oflow_conv_s32_ex4(const void* d_x, long long x_pixel_stride, int in_groups,
                        long long res_pixel_stride, int res_activation, int s2d, int in_format,
                        const float* d_in_scale, const float* d_in_shift, const float* d_addend,
                        long long addend_pixel_stride, const void* d_wfrag, void* stream);
+/* oflow_conv_s32_ex5: oflow_conv_s32_ex4 plus split-K over the input groups for the register-direct kernels (S32 input,
+ * d_wfrag given, in_groups even; the 224-workgroup GRU q / motion convs of a 4-pair lane fill 224 of 512 two-per-CU
+ * slots unsplit). Each 4 x 32-pixel tile (x block_n channels) runs as two workgroups, each summing half of the input
+ * groups; the first to finish hands its fp32 partials to the second through d_ksplit_slab (write-through stores, an
+ * agent-scope counter, an acquire on the reader), which adds them and runs the epilogue. Results differ from ex4 only
+ * in the order of one fp32 addition per output (and do not depend on which workgroup finishes first).
+ *   d_ksplit_slab: >= ksplit_tiles * 128 * block_n floats, 16-B aligned, any contents;
+ *   d_ksplit_ctr: 2 * ksplit_tiles uint32, 8-B aligned, ZEROED ONCE before the first call; the counters only grow (two
+ *     tickets and one publication per tile and call), so successive calls and graph replays need no reset -- but
+ *     calls that share a buffer pair must be stream-ordered (never in flight together);
+ *   ksplit_tiles: capacity; OFLOW_E_SHAPE if the call needs B * ceil(H/4) * ceil(W/32) * n_pad / block_n more.
+ * A split call always runs the default 4-row tiles, small grids included (so that a caller deciding the split from its
+ * whole batch gets the same bits from any partition of it into calls); calls of other shapes (not register-direct, odd
+ * in_groups) run unsplit. Both NULL = ex4. */
+int oflow_conv_s32_ex5(const void* d_x, long long x_pixel_stride, int in_groups, const void* d_wpack, int n_pad,
+                       const float* d_wscale, const float* d_bias, int N, int B, int H, int W, int kh, int kw,
+                       int block_n, int epilogue, int activation, float out_scale, void* d_y0, long long y0_pixel_stride,
+                       void* d_y1, long long y1_pixel_stride, float* d_f32, long long f32_batch_stride,
+                       long long f32_channel_stride, int f32_accumulate, float* d_gru_h, float* d_gru_z,
+                       int gru_channels, float* d_nhwc, int nhwc_pixel_stride, float* d_stats, const void* d_res,
+                       long long res_pixel_stride, int res_activation, int s2d, int in_format,
+                       const float* d_in_scale, const float* d_in_shift, const float* d_addend,
+                       long long addend_pixel_stride, const void* d_wfrag, float* d_ksplit_slab,
+                       unsigned* d_ksplit_ctr, long long ksplit_tiles, void* stream);
 int oflow_stem_patches_s32(const float* d_img, int B, int C, int H, int W, void* d_out, int out_groups, void* stream);
 int oflow_norm_stats_finalize(const float* d_partials, int B, int tiles, int n_pad, int C, double eps, float* d_alpha,
                               float* d_beta, void* stream);

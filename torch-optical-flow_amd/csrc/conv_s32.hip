@@ -120,6 +120,11 @@ struct ConvArgs {
   int wbytes;              // bytes of the packed weights (kg * taps * npad * 128)
   const uint8_t* wf;       // the same weights fragment-major (register-direct B, BREG kernels), or null
   int exp_flags;           // experiments only (oflow_exp_set_conv_flags): bit 0 = the stem's element-wise window loop
+  // split-K (BREG kernels only, oflow_conv_s32_ex5): gridDim.z = 2 workgroups per tile, each summing half of the input
+  // groups (kg above is the half); per tile a BM x BN fp32 partial slab and two counters [ticket, published]
+  float* ks_slab;
+  unsigned* ks_ctr;
+  long long ks_tiles;      // tiles (x channel blocks) the slab and counters hold
 };
 // input formats of oflow_conv_s32_ex2
 constexpr int kInS32 = OFLOW_IN_S32, kInF32Norm = OFLOW_IN_F32_NORM, kInF32 = OFLOW_IN_F32, kInImg = OFLOW_IN_IMG7S2,
@@ -263,6 +268,13 @@ __global__ __launch_bounds__(64 * WM * WN, WM * WN == 8 ? 1 : 2) void conv_s32_k
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave / WN, wn = wave % WN;
   const int r = lane & 31, hh = lane >> 5;
+  if constexpr (BREG) {
+    if (a.ks_slab != nullptr) {  // split-K: this workgroup's half of the input groups (a.kg is the half count)
+      const int z = blockIdx.z;
+      a.x += (long long)z * a.kg * 128;                 // S32 channel slice: + 128 B per group
+      a.wf += (long long)z * a.kg * T * a.npad * 128;   // fragment-major weights are step-major, step = (group, tap)
+    }
+  }
   auto aswz = [](int p) { return (BREG || OFLOW_PAD_ROWS) ? 0 : swz(p); };  // row slot swizzles (none with padded rows)
   auto bswz = [](int n) { return OFLOW_PAD_ROWS ? 0 : swz(n); };
 
@@ -726,6 +738,71 @@ __global__ __launch_bounds__(64 * WM * WN, WM * WN == 8 ? 1 : 2) void conv_s32_k
 #undef OFLOW_LOAD_B
 #undef OFLOW_WRITE_B
 
+  if constexpr (BREG) {
+    if (a.ks_slab != nullptr) {
+      // Split-K hand-off (MI355X_MICROARCH.md "inter-workgroup visibility"; cdna_hip_programming.md Guideline 16 R1):
+      // the tile's two workgroups take tickets from one counter; the first publishes its partial sums write-through
+      // (16-B sc1 stores: no release fence), drains them, and one lane bumps the tile's "published" counter; the second
+      // polls that counter (relaxed agent-scope loads), drops its L1 with one agent acquire and adds the partials to its
+      // own before running the epilogue. fp32 addition is commutative, so acc_0 + acc_1 is the same bits whichever
+      // workgroup arrives second. Counters only grow (two tickets and one publication per tile and launch), so they
+      // need no reset between launches or graph replays; the host zeroes them once. The second arriver polls only after
+      // the first took its ticket (it is resident and past its main loop): no dependence on dispatch order. The poll is
+      // bounded (a hang would hold the GPU): past the bound it proceeds without the partials (the results are then
+      // wrong, which the parity tests see).
+      typedef __attribute__((address_space(1))) unsigned gu32;
+      __shared__ unsigned sTicket;
+      const int tile_id = blockIdx.y * gridDim.x + blockIdx.x;
+      gu32* ctr = (gu32*)(a.ks_ctr) + 2 * tile_id;  // (global address space: no flat atomics)
+      if (tid == 0) sTicket = __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __syncthreads();
+      const unsigned ticket = sTicket;
+      // slab of the tile: [wave][mt][nt][16-B quarter of the accumulator][lane 64][16 B] (one wave instruction = 1 KB)
+      const __amdgpu_buffer_rsrc_t rsS = __builtin_amdgcn_make_buffer_rsrc(
+          a.ks_slab + (size_t)tile_id * (BM * BN), (short)0, BM * BN * 4, 0x00020000);
+      const int sbase = wave * (MT * NT * 4096) + lane * 16;
+      if ((ticket & 1u) == 0u) {
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+          for (int nt = 0; nt < NT; ++nt)
+#pragma unroll
+            for (int e4 = 0; e4 < 4; ++e4) {
+              const u32x4 v = {__float_as_uint(acc[mt][nt][4 * e4]), __float_as_uint(acc[mt][nt][4 * e4 + 1]),
+                               __float_as_uint(acc[mt][nt][4 * e4 + 2]), __float_as_uint(acc[mt][nt][4 * e4 + 3])};
+              __builtin_amdgcn_raw_buffer_store_b128(v, rsS, sbase + ((mt * NT + nt) * 4 + e4) * 1024, 0, 16);  // sc1
+            }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains its write-through stores
+        __syncthreads();
+        if (tid == 0) __hip_atomic_fetch_add(ctr + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        return;
+      }
+      if (tid == 0) {
+        const unsigned want = (ticket >> 1) + 1u;
+        for (unsigned spin = 0; spin < (1u << 24); ++spin) {
+          if (static_cast<int>(__hip_atomic_load(ctr + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - want) >= 0) break;
+          __builtin_amdgcn_s_sleep(1);
+        }
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+      __syncthreads();
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt) {
+          u32x4 pv[4];
+#pragma unroll
+          for (int e4 = 0; e4 < 4; ++e4)
+            pv[e4] = __builtin_amdgcn_raw_buffer_load_b128(rsS, sbase + ((mt * NT + nt) * 4 + e4) * 1024, 0, 0);
+#pragma unroll
+          for (int e4 = 0; e4 < 4; ++e4)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) acc[mt][nt][4 * e4 + j] += __uint_as_float(pv[e4][j]);
+        }
+    }
+  }
+
   // ---- epilogue: accumulators -> LDS tile [pixel][channel] ----
   constexpr int C8 = BN / 8;
   constexpr int KIT = (BM * C8 + NTH - 1) / NTH;  // epilogue items (pixel x 8 channels) per thread
@@ -1041,6 +1118,10 @@ int launch_conv(const ConvArgs& a0, hipStream_t s) {
   if constexpr (BREG) {
     a.tiles_y = (a.H + TY - 1) / TY;
     dim3 grid = conv_grid(a, BN);
+    if (a.ks_slab != nullptr) {
+      if (OFLOW_XCD_MAP || (long long)grid.x * grid.y > a.ks_tiles) return OFLOW_E_SHAPE;
+      grid.z = 2;
+    }
     hipLaunchKernelGGL((conv_s32_kernel<KH, KW, BN, WM, WN, EPI, TY, kInS32, true>), grid, dim3(64 * WM * WN), 0, s, a);
     return launch_status();
   } else {
@@ -1098,9 +1179,11 @@ int g_bn64_8row = 0;
 // -> 144.8 / 149.9 us, step 18.96 -> 19.74 ms (profiles/r04/s26_*) -- with one workgroup per CU each halo-swap
 // barrier idles the CU's matrix cores; 128-channel 8-wave workgroups (2 x 4 of 2 row tiles, <= 128 VGPRs, four waves
 // per SIMD): z|r 141.0 / 141.1 -> 148.9 / 150.3 us, step 19.07 -> 19.65 ms (s27_*).
+// (a split-K call always takes the default tiles: the caller decides the split from its whole batch, so that pair
+// lanes of a forward compute what one lane computes, bit for bit, whatever their own sizes)
 inline bool small_grid(const ConvArgs& a, int bn) {
   return (long long)a.B * a.H * a.W < g_small_grid_px && a.stats == nullptr && a.ain == kInS32 && a.npad % 64 == 0 &&
-         bn >= 64;
+         bn >= 64 && a.ks_slab == nullptr;
 }
 
 // register-direct weights (BREG): 128-channel blocks of T > 1 convs on S32 input, given the fragment-major weights.
@@ -1259,6 +1342,17 @@ OFLOW_RANGE_FLAG_SETTER(conv)
 
 using namespace oflow;
 
+extern "C" int oflow_conv_s32_ex5(const void* d_x, long long x_pixel_stride, int in_groups, const void* d_wpack,
+                                  int n_pad, const float* d_wscale, const float* d_bias, int N, int B, int H, int W, int kh,
+                                  int kw, int block_n, int epilogue, int activation, float out_scale, void* d_y0,
+                                  long long y0_pixel_stride, void* d_y1, long long y1_pixel_stride, float* d_f32,
+                                  long long f32_batch_stride, long long f32_channel_stride, int f32_accumulate,
+                                  float* d_gru_h, float* d_gru_z, int gru_channels, float* d_nhwc, int nhwc_pixel_stride,
+                                  float* d_stats, const void* d_res, long long res_pixel_stride, int res_activation,
+                                  int s2d, int in_format, const float* d_in_scale, const float* d_in_shift,
+                                  const float* d_addend, long long addend_pixel_stride, const void* d_wfrag,
+                                  float* d_ksplit_slab, unsigned* d_ksplit_ctr, long long ksplit_tiles, void* stream);
+
 extern "C" int oflow_conv_s32_ex4(const void* d_x, long long x_pixel_stride, int in_groups, const void* d_wpack,
                                   int n_pad, const float* d_wscale, const float* d_bias, int N, int B, int H, int W, int kh,
                                   int kw, int block_n, int epilogue, int activation, float out_scale, void* d_y0,
@@ -1268,6 +1362,23 @@ extern "C" int oflow_conv_s32_ex4(const void* d_x, long long x_pixel_stride, int
                                   float* d_stats, const void* d_res, long long res_pixel_stride, int res_activation,
                                   int s2d, int in_format, const float* d_in_scale, const float* d_in_shift,
                                   const float* d_addend, long long addend_pixel_stride, const void* d_wfrag, void* stream) {
+  return oflow_conv_s32_ex5(d_x, x_pixel_stride, in_groups, d_wpack, n_pad, d_wscale, d_bias, N, B, H, W, kh, kw,
+                            block_n, epilogue, activation, out_scale, d_y0, y0_pixel_stride, d_y1, y1_pixel_stride,
+                            d_f32, f32_batch_stride, f32_channel_stride, f32_accumulate, d_gru_h, d_gru_z, gru_channels,
+                            d_nhwc, nhwc_pixel_stride, d_stats, d_res, res_pixel_stride, res_activation, s2d, in_format,
+                            d_in_scale, d_in_shift, d_addend, addend_pixel_stride, d_wfrag, nullptr, nullptr, 0, stream);
+}
+
+extern "C" int oflow_conv_s32_ex5(const void* d_x, long long x_pixel_stride, int in_groups, const void* d_wpack,
+                                  int n_pad, const float* d_wscale, const float* d_bias, int N, int B, int H, int W, int kh,
+                                  int kw, int block_n, int epilogue, int activation, float out_scale, void* d_y0,
+                                  long long y0_pixel_stride, void* d_y1, long long y1_pixel_stride, float* d_f32,
+                                  long long f32_batch_stride, long long f32_channel_stride, int f32_accumulate,
+                                  float* d_gru_h, float* d_gru_z, int gru_channels, float* d_nhwc, int nhwc_pixel_stride,
+                                  float* d_stats, const void* d_res, long long res_pixel_stride, int res_activation,
+                                  int s2d, int in_format, const float* d_in_scale, const float* d_in_shift,
+                                  const float* d_addend, long long addend_pixel_stride, const void* d_wfrag,
+                                  float* d_ksplit_slab, unsigned* d_ksplit_ctr, long long ksplit_tiles, void* stream) {
   ConvArgs a;
   const int st = build_conv_args(a, d_x, x_pixel_stride, in_groups, d_wpack, n_pad, d_wscale, d_bias, N, B, H, W, kh, kw,
                                  block_n, epilogue, activation, out_scale, d_y0, y0_pixel_stride, d_y1, y1_pixel_stride,
@@ -1319,6 +1430,31 @@ extern "C" int oflow_conv_s32_ex4(const void* d_x, long long x_pixel_stride, int
     if (((uintptr_t)d_addend & 15) || (addend_pixel_stride & 3) || addend_pixel_stride < N) return OFLOW_E_ALIGN;
     a.add = d_addend;
     a.addps = addend_pixel_stride;
+  }
+  if (d_ksplit_slab || d_ksplit_ctr) {
+    // split-K over the input groups: only the register-direct kernels (S32 input, fragment-major weights, multi-tap,
+    // 4-row tiles) take it; any other path this call would dispatch to runs unsplit (same results up to the order of
+    // one fp32 addition per output)
+    if (!d_ksplit_slab || !d_ksplit_ctr) return OFLOW_E_NULL;
+    if (((uintptr_t)d_ksplit_slab & 15) || ((uintptr_t)d_ksplit_ctr & 7)) return OFLOW_E_ALIGN;
+    if (ksplit_tiles <= 0) return OFLOW_E_SHAPE;
+    // (the register-direct instances: launch_bn / dispatch_conv -- 128-channel blocks of any multi-tap kernel but 2x2,
+    // 64- and 32-channel blocks of 3x3 ones; the GRU epilogues 1x5 / 5x1 only -- at the default tiles whatever the
+    // grid's size, see small_grid)
+    a.ks_slab = d_ksplit_slab;
+    const bool breg = in_format == kInS32 && a.wf != nullptr && use_breg(a, block_n, kh * kw) && kh * kw != 4 &&
+                      (block_n == 128 || (kh == 3 && kw == 3)) && (epilogue == 0 || kh * kw == 5);
+    a.ks_slab = nullptr;
+    if (breg && (in_groups % 2) == 0) {
+      // ksplit_tiles: the slab's capacity in (4 x 32-pixel tile, block_n channels) units of 128 * block_n floats
+      if ((long long)B * ((H + kTY - 1) / kTY) * ((W + kTX - 1) / kTX) * (n_pad / block_n) > ksplit_tiles)
+        return OFLOW_E_SHAPE;
+      a.ks_slab = d_ksplit_slab;
+      a.ks_ctr = d_ksplit_ctr;
+      a.ks_tiles = ksplit_tiles;
+      a.kg = in_groups / 2;
+      a.wbytes /= 2;
+    }
   }
   return dispatch_conv(a, kh, kw, block_n, epilogue, static_cast<hipStream_t>(stream));
 }

@@ -79,6 +79,17 @@ FLOW_HEAD_MODE = _env_choice("OFLOW_FLOW_HEAD_MODE", "tiled", ("tiled", "conv", 
 # builds the patch operand in LDS) from this many pixels of the whole forward's batch up; below it flow_prep writes the
 # patch matrix and convf1 runs on the small-grid tiles. Bit-identical either way (same patch values, same k order).
 CONVF1_FROM_FLOW_MIN_PIXELS = 16384 if _env_choice("OFLOW_CONVF1_FROM_FLOW", "1", ("0", "1")) == "1" else 1 << 62  # (0: A/B)
+# r06: split-K (oflow_conv_s32_ex5) for the update convs whose lane launch fills fewer than half of the chip's
+# two-per-CU workgroup slots: the motion conv ("mo", 3x3 256 -> 126) and both GRU candidate convs ("q", 1x5 / 5x1
+# 256 -> 128) run 224 workgroups per 4-pair lane unsplit. Each tile's two workgroups sum half of the input groups and
+# meet through an fp32 slab (csrc/conv_s32.hip). Decided from the whole forward's pixel count (as the flow head's
+# kernel), so pair lanes keep giving the single-lane flows bit for bit. Measured on the replayed 8-pair graph
+# (tools/exp/run_graph_ab.py, profiles/r06/r6s12_ab.log, one box, alternated): unsplit 17.73 ms/step, both layers split
+# 18.21, q only 17.75, motion only 18.17 -- the other lane's kernels already fill the CUs the 224-workgroup launches
+# leave idle, and the split adds a slab round trip and a second workgroup per tile. So the default is unsplit; the
+# ex5 path stays for callers whose launches run alone (tests/test_gpu_conv_ksplit.py). e.g. {"mo", "q"} to enable.
+KSPLIT_LAYERS = frozenset()
+KSPLIT_MIN_PIXELS = 16384
 
 class FlowHead(nn.Module):
     def __init__(self, input_dim: int = 128, hidden_dim: int = 256) -> None:
@@ -351,6 +362,10 @@ class SplitUpdate:
         px = b * h * w if flow_head_pixels is None else int(flow_head_pixels)
         self.flow_head_fma = px < _native.FLOW_HEAD2_MAX_PIXELS
         self.f1_from_flow = px >= CONVF1_FROM_FLOW_MIN_PIXELS
+        # split-K scratch, one per runner (the calls sharing it are ordered on this runner's stream)
+        self.ks = _native.KSplit(b, h, w, dev) if KSPLIT_LAYERS and px >= KSPLIT_MIN_PIXELS else None
+        self.ks_mo = self.ks if "mo" in KSPLIT_LAYERS else None
+        self.ks_q = self.ks if "q" in KSPLIT_LAYERS else None
         S = _native.s32_empty
         self.hx = S(b, h, w, 8, dev)
         self.rhx = S(b, h, w, 8, dev)
@@ -489,12 +504,12 @@ class SplitUpdate:
             conv(V(self.c1), w["c2"], bns["c2"], "relu", y0=V(self.cf, 0, 6))
             conv(f1_in, w["f1"], bns["f1"], "relu", y0=V(self.f1))
             conv(V(self.f1), w["f2"], bns["f2"], "relu", y0=V(self.cf, 6, 2))
-        conv(V(self.cf), w["mo"], bns["mo"], "relu", y0=V(self.hx, 4, 4), y1=V(self.rhx, 4, 4))
+        conv(V(self.cf), w["mo"], bns["mo"], "relu", y0=V(self.hx, 4, 4), y1=V(self.rhx, 4, 4), ksplit=self.ks_mo)
         for tag, gx in zip(("1", "2"), self.gx):
             conv(V(self.hx), w["zr" + tag], bns["gru"], epilogue=1, y0=V(self.rhx, 0, 4), gru_h=self.hm, gru_z=self.z,
                  addend=gx[:, :256])
             conv(V(self.rhx), w["q" + tag], bns["gru"], epilogue=2, y0=V(self.hx, 0, 4), gru_h=self.hm, gru_z=self.z,
-                 addend=gx[:, 256:])
+                 addend=gx[:, 256:], ksplit=self.ks_q)
         net = V(self.hx, 0, 4)
         conv(net, w["fh1"], bns["fh1"], "relu", y0=V(self.fh))
         if self.flow_head_fma and coords1.is_contiguous():

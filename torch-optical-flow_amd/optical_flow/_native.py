@@ -70,6 +70,7 @@ SYMBOLS = (
     "oflow_flow_head2_tiled_s32",
     "oflow_conv_s32_ex3",
     "oflow_conv_s32_ex4",
+    "oflow_conv_s32_ex5",
     "oflow_normalize_images_f32",
     "oflow_replicate_pad_f32",
     "oflow_corr_fmap_grad_f32",
@@ -246,6 +247,8 @@ def load() -> ctypes.CDLL:
     lib.oflow_replicate_pad_f32.restype = I
     lib.oflow_replicate_pad_f32.argtypes = [P, P, I, L, I, I, I, I, I, I, P]
     lib.oflow_conv_s32_ex4.argtypes = list(lib.oflow_conv_s32_ex3.argtypes[:-1]) + [P, P]
+    lib.oflow_conv_s32_ex5.restype = I
+    lib.oflow_conv_s32_ex5.argtypes = list(lib.oflow_conv_s32_ex4.argtypes[:-1]) + [P, P, L, P]
     lib.oflow_corr_lookup_backward_f32.restype = I
     lib.oflow_corr_lookup_backward_f32.argtypes = [P, P, I, I, I, I, PP, IP, IP, I, P]
     lib.oflow_corr_pyramid_grad_combine_f32.restype = I
@@ -1029,15 +1032,28 @@ def conv_tiles(h: int, w: int) -> int:
     return ((h + 3) // 4) * ((w + 31) // 32)
 
 
+class KSplit:
+    """Split-K scratch for oflow_conv_s32_ex5 (include/oflow.h): an fp32 partial slab of ``tiles`` (4 x 32-pixel tile,
+    128-channel block) units and its [ticket, published] counters, zeroed here once. Calls sharing one KSplit must be
+    stream-ordered (one per update lane)."""
+
+    def __init__(self, b: int, h: int, w: int, device, block_n: int = 128, blocks: int = 1) -> None:
+        self.tiles = b * conv_tiles(h, w) * blocks  # (blocks: channel blocks of block_n per tile)
+        self.block_n = block_n
+        self.slab = torch.empty(self.tiles * 128 * block_n, device=device, dtype=torch.float32)
+        self.ctr = torch.zeros(2 * self.tiles, device=device, dtype=torch.int32)
+
+
 def conv_s32(x: S32Slice, cw: ConvWeights, block_n: int, act: str = "none", out_scale: float = 1.0, y0=None, y1=None,
              f32=None, f32_accumulate: bool = False, epilogue: int = 0, gru_h=None, gru_z=None, nhwc=None, stats=None,
-             res=None, res_act: str = "none", s2d: bool = False, addend=None) -> None:
-    """Split-fp16 convolution (oflow_conv_s32_ex4). x: input S32Slice with cw.kg groups, or NhwcNormIn (3x3 only). y0/y1: S32Slice destinations
+             res=None, res_act: str = "none", s2d: bool = False, addend=None, ksplit: "KSplit" = None) -> None:
+    """Split-fp16 convolution (oflow_conv_s32_ex5). x: input S32Slice with cw.kg groups, or NhwcNormIn (3x3 only). y0/y1: S32Slice destinations
     (s2d: space-to-depth layout, half the spatial size). f32: (B, N', H, W) fp32 NCHW destination. nhwc: [P, N]
     fp32 destination. stats: instance-norm partials [B, conv_tiles(H, W), n_pad, 3]. res: S32Slice residual added
     after the activation, then res_act. epilogue 1/2: GRU gates / candidate with gru_h, gru_z ([P, CH] fp32);
     addend: fp32 [P, >= N] (row stride a multiple of 4, 16-B aligned) added before the gate activations (the GRU's
-    hoisted context term)."""
+    hoisted context term). ksplit: split-K scratch (KSplit) -- the register-direct kernels then run each tile as two
+    workgroups over half the input groups each (one more fp32 addition per output); other kernels ignore it."""
     what = "conv_s32"
     if CHECK_RANGE:
         _range_check(x, f"{what} {cw.kh}x{cw.kw}")
@@ -1089,9 +1105,16 @@ def conv_s32(x: S32Slice, cw: ConvWeights, block_n: int, act: str = "none", out_
         taps, p_out = cw.kh * cw.kw, b * h * w  # (s2d only changes where the epilogue writes)
         n_exec = -(-cw.n_pad // int(block_n)) * int(block_n)
         _count(3 * 2 * p_out * n_exec * cw.kg * 32 * taps, 2 * p_out * cw.n * cw.cin * taps)
+    ks_slab = ks_ctr = None
+    ks_tiles = 0
+    if ksplit is not None and wf is not None:
+        if ksplit.slab.device != dev or ksplit.block_n < int(block_n):
+            raise RuntimeError(f"{what}: split-K scratch on another device or for narrower channel blocks")
+        ks_slab, ks_ctr = ksplit.slab.data_ptr(), ksplit.ctr.data_ptr()
+        ks_tiles = ksplit.tiles * (ksplit.block_n // int(block_n))
     with torch.cuda.device(dev), _Timed(f"conv{cw.kh}x{cw.kw}", dev):
         _check(
-            load().oflow_conv_s32_ex4(
+            load().oflow_conv_s32_ex5(
                 x.ptr, x.ps, cw.kg, cw.pack.data_ptr(), cw.n_pad, cw.wscale.data_ptr(),
                 cw.bias.data_ptr() if cw.bias is not None else None, cw.n, b, h, w, cw.kh, cw.kw, int(block_n),
                 int(epilogue), ACT[act], float(out_scale), y0.ptr if y0 is not None else None, y0.ps if y0 is not None else 0,
@@ -1101,7 +1124,7 @@ def conv_s32(x: S32Slice, cw: ConvWeights, block_n: int, act: str = "none", out_
                 stats.data_ptr() if stats is not None else None,
                 res.ptr if res is not None else None, res.ps if res is not None else 0, ACT[res_act], int(bool(s2d)),
                 in_format, x.scale.data_ptr() if nin else None, x.shift.data_ptr() if nin else None,
-                ap or None, aps, wf, _stream(dev),
+                ap or None, aps, wf, ks_slab, ks_ctr, ks_tiles, _stream(dev),
             ),
             what,
         )
