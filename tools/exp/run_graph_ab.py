@@ -5,7 +5,9 @@ the first variant's.
 
     VARIANTS='off:update.KSPLIT_LAYERS=frozenset();on:update.KSPLIT_LAYERS=frozenset({"mo","q"})' \
         python tools/exp/run_graph_ab.py
-Each variant is "name:module.ATTR=python-expression[,module.ATTR=...]" over the modules of methods/raft/model."""
+Each variant is "name:module.ATTR=python-expression[,,module.ATTR=...]" over the modules of methods/raft/model, or
+"lib.oflow_exp_set_X=V/R": liboflow's int experiment setter, V during the capture, R after it."""
+import ctypes
 import importlib
 import json
 import os
@@ -20,6 +22,20 @@ import torch  # noqa: E402
 
 from model import RAFT, InputPadder, synthetic  # noqa: E402
 from model import graph as G  # noqa: E402
+from optical_flow import _native  # noqa: E402
+
+
+class _Lib:
+    """lib.oflow_exp_set_X=V/R: the library's int setter, called with V for the capture and R after it."""
+
+    def __init__(self):
+        self.vals = {}
+
+    def set(self, name, v):
+        fn = getattr(_native.load(), name)
+        fn.argtypes, fn.restype = [ctypes.c_int], None
+        fn(int(v))
+        self.vals[name] = v
 
 
 def parse(spec):
@@ -30,7 +46,11 @@ def parse(spec):
         for a in filter(None, sets.split(",,")):
             lhs, _, rhs = a.partition("=")
             mod, _, attr = lhs.strip().rpartition(".")
-            assigns.append((importlib.import_module("model." + mod), attr, eval(rhs)))  # noqa: S307 (experiment tool)
+            if mod == "lib":
+                v, _, r = rhs.partition("/")
+                assigns.append(("lib", attr, (int(v), int(r or 0))))
+            else:
+                assigns.append((importlib.import_module("model." + mod), attr, eval(rhs)))  # noqa: S307 (experiment tool)
         out.append((name, assigns))
     return out
 
@@ -50,16 +70,23 @@ def main():
     p0, p1 = padder.pad(a0.to(dev).repeat(r, 1, 1, 1)[:pairs], a1.to(dev).repeat(r, 1, 1, 1)[:pairs])
     graphs, flows = {}, {}
     with torch.inference_mode():
+        lib = _Lib()
         for name, assigns in variants:
-            saved = [(m, at, getattr(m, at)) for m, at, _ in assigns]
+            saved = [(m, at, getattr(m, at)) for m, at, _ in assigns if m != "lib"]
             for m, at, v in assigns:
-                setattr(m, at, v)
+                if m == "lib":
+                    lib.set(at, v[0])
+                else:
+                    setattr(m, at, v)
             try:
                 graphs[name] = G.GraphedRAFT(model, p0, p1, iters=12)
                 flows[name] = graphs[name](p0, p1)[1].clone()
             finally:
                 for m, at, v in saved:
                     setattr(m, at, v)
+                for m, at, v in assigns:
+                    if m == "lib":
+                        lib.set(at, v[1])
         torch.cuda.synchronize()
         times = {n: [] for n in graphs}
         for _ in range(rounds):

@@ -202,7 +202,11 @@ __device__ __forceinline__ void store_s32(uint8_t* y, long long ps, long long P,
 // no B staging through LDS, and the only barriers are the two around each input group's halo swap (T steps per group
 // instead of one barrier per step). No two waves load the same fragment. Same MFMAs in the same order per accumulator
 // as the LDS-staged kernel: bit-identical outputs.
-template <int KH, int KW, int BN, int WM, int WN, int EPI, int TY = kTY, int AIN = kInS32, bool BREG = false>
+// BD (LDS-staged B, r06): steps of operand prefetch in registers -- B(i + BD) is loaded at step i into one of BD
+// register sets (1x1 convs: A too). With BD = 1 the load issued just before a step's barrier was written to LDS a
+// few MFMAs into the next step (an L2 round trip of ~0.3-0.5 us waited out in most steps: s_waitcnt vmcnt(0) in the
+// main loop's ISA); BD = 2 (launch_staged, the default) gives it a whole step more.
+template <int KH, int KW, int BN, int WM, int WN, int EPI, int TY = kTY, int AIN = kInS32, bool BREG = false, int BD = 1>
 // (the second bound is HIP's minimum waves per SIMD: 2 -> <= 256 VGPRs)
 __global__ __launch_bounds__(64 * WM * WN, WM * WN == 8 ? 1 : 2) void conv_s32_kernel(ConvArgs a) {
   constexpr int NTH = 64 * WM * WN;  // 4 waves (two workgroups per CU) or 8 (one)
@@ -678,20 +682,20 @@ __global__ __launch_bounds__(64 * WM * WN, WM * WN == 8 ? 1 : 2) void conv_s32_k
 #undef OFLOW_READ_A
 #undef OFLOW_MFMAS_R
   } else {
-  // prologue: step 0 in LDS, step 1 in registers, sub-step 0 operands of step 0 read
-  OFLOW_LOAD_B(rb, 0);
-  OFLOW_LOAD_A(ra, 0);
-  OFLOW_WRITE_A(ra, 0, 0);
-  OFLOW_WRITE_B(rb, 0);
-  {
-    const int i1 = S > 1 ? 1 : 0;
-    OFLOW_LOAD_B(rb, i1);
-    if constexpr (ADB) {
-      OFLOW_LOAD_A(ra, i1);
-    } else {
-      OFLOW_LOAD_A(ra, a.kg > 1 ? 1 : 0);
-    }
+  // prologue: step 0 in LDS, steps 1 .. BD in registers (set d % BD), sub-step 0 operands of step 0 read
+  u32x4 rbr[BD][BPER];
+  u32x4 rar[ADB ? BD : 1][APER];
+  OFLOW_LOAD_B(rbr[0], 0);
+  OFLOW_LOAD_A(rar[0], 0);
+  OFLOW_WRITE_A(rar[0], 0, 0);
+  OFLOW_WRITE_B(rbr[0], 0);
+#pragma unroll
+  for (int d = 1; d <= BD; ++d) {
+    const int id = d < S ? d : S - 1;
+    OFLOW_LOAD_B(rbr[d % BD], id);
+    if constexpr (ADB) { OFLOW_LOAD_A(rar[d % BD], id); }
   }
+  if constexpr (!ADB) { OFLOW_LOAD_A(rar[0], a.kg > 1 ? 1 : 0); }
   __syncthreads();
   half8 xah[MT], xal[MT], xbh[NT], xbl[NT];  // sub-step 0 operands
   half8 yah[MT], yal[MT], ybh[NT], ybl[NT];  // sub-step 1 operands
@@ -700,17 +704,23 @@ __global__ __launch_bounds__(64 * WM * WN, WM * WN == 8 ? 1 : 2) void conv_s32_k
   // The loop body is one input group with its T taps unrolled (static tap index), and nothing in it is conditional:
   // past the last step it re-loads / re-writes the last step's data into buffers no longer read, so the compiler
   // sees every load and counts vmcnt exactly (a halo prefetch from HBM is never waited for by a weight write).
-  for (int g = 0; g < a.kg; ++g) {
+  // (a body of GPB2 groups keeps the register set of every step static: (i + 1) % BD = (j + 1) % BD)
+  constexpr int GPB2 = (BD > 1 && (T % BD) != 0) ? BD : 1;
+  for (int g0 = 0; g0 < a.kg; g0 += GPB2) {
 #pragma unroll
-    for (int t = 0; t < T; ++t) {
+    for (int j = 0; j < GPB2 * T; ++j) {
+      const int g = g0 + j / T, t = j % T;
+      if (GPB2 > 1 && j > 0 && t == 0 && g >= a.kg) break;  // the last body's missing groups (uniform branch)
       const int i_ = g * T + t;
-      // 1-2: step i+1's operands into the LDS buffers step i-1 used (free since step i-1's barrier); reload
+      u32x4 (&rb)[BPER] = rbr[(j + 1) % BD];
+      // 1-2: step i+1's operands into the LDS buffers step i-1 used (free since step i-1's barrier); reload the
+      // register set with step i+1+BD's
       OFLOW_WRITE_B(rb, (i_ + 1) & 1);
-      if constexpr (ADB) { OFLOW_WRITE_A(ra, (i_ + 1) & 1, i_ + 1 < S ? i_ + 1 : S - 1); }
+      if constexpr (ADB) { OFLOW_WRITE_A(rar[(j + 1) % BD], (i_ + 1) & 1, i_ + 1 < S ? i_ + 1 : S - 1); }
       {
-        const int i2 = i_ + 2 < S ? i_ + 2 : S - 1;
+        const int i2 = i_ + 1 + BD < S ? i_ + 1 + BD : S - 1;
         OFLOW_LOAD_B(rb, i2);
-        if constexpr (ADB) { OFLOW_LOAD_A(ra, i2); }
+        if constexpr (ADB) { OFLOW_LOAD_A(rar[(j + 1) % BD], i2); }
       }
       // 3-4
       OFLOW_READ_OPS(yah, yal, ybh, ybl, i_, 1);
@@ -719,9 +729,9 @@ __global__ __launch_bounds__(64 * WM * WN, WM * WN == 8 ? 1 : 2) void conv_s32_k
       if constexpr (!ADB) {
         if (t == T - 1) {
           __syncthreads(); /* every wave is done reading A(g) */
-          OFLOW_WRITE_A(ra, 0, g + 1 < a.kg ? g + 1 : g);
+          OFLOW_WRITE_A(rar[0], 0, g + 1 < a.kg ? g + 1 : g);
           const int g2 = g + 2 < a.kg ? g + 2 : a.kg - 1;
-          OFLOW_LOAD_A(ra, g2);
+          OFLOW_LOAD_A(rar[0], g2);
         }
       }
       if (!OFLOW_ABL(64)) __syncthreads(); /* B(i+1) [A] visible; every read of step i done before step i+1 overwrites its buffers */
@@ -1112,6 +1122,15 @@ inline dim3 conv_grid(const ConvArgs& a, int bn) {
   return OFLOW_XCD_MAP ? dim3(ntiles * (a.npad / bn)) : dim3(ntiles, a.npad / bn);
 }
 
+// LDS-staged kernels: operands prefetched two steps ahead (BD 2). r06 in-process A/B on the replayed 8-pair graph,
+// alternated (tools/exp/run_graph_ab.py, profiles/r06/r6s16_ab.log): 17.883 (BD 1) -> 17.720 ms/step, bit-identical
+// (the same MFMAs in the same order; only the loads move). The loop's ISA has no s_waitcnt vmcnt(0) left (7-9 per
+// input group with BD 1).
+template <int KH, int KW, int BN, int WM, int WN, int EPI, int TY, int AIN>
+void launch_staged(const ConvArgs& a, dim3 grid, hipStream_t s) {
+  hipLaunchKernelGGL((conv_s32_kernel<KH, KW, BN, WM, WN, EPI, TY, AIN, false, 2>), grid, dim3(64 * WM * WN), 0, s, a);
+}
+
 template <int KH, int KW, int BN, int WM, int WN, int EPI, int TY = kTY, bool BREG = false>
 int launch_conv(const ConvArgs& a0, hipStream_t s) {
   ConvArgs a = a0;
@@ -1129,30 +1148,30 @@ int launch_conv(const ConvArgs& a0, hipStream_t s) {
   dim3 grid = conv_grid(a, BN);
   if constexpr (KH == 3 && KW == 3 && EPI == 0) {  // the encoders' second block convs
     if (a.ain == kInF32Norm) {
-      hipLaunchKernelGGL((conv_s32_kernel<KH, KW, BN, WM, WN, EPI, TY, kInF32Norm>), grid, dim3(64 * WM * WN), 0, s, a);
+      launch_staged<KH, KW, BN, WM, WN, EPI, TY, kInF32Norm>(a, grid, s);
       return launch_status();
     }
   }
   if constexpr (KH == 1 && KW == 1 && EPI == 0 && BN == 64 && TY == kTY) {  // the encoders' stem from the image
     if (a.ain == kInImg) {
-      hipLaunchKernelGGL((conv_s32_kernel<KH, KW, BN, WM, WN, EPI, TY, kInImg>), grid, dim3(64 * WM * WN), 0, s, a);
+      launch_staged<KH, KW, BN, WM, WN, EPI, TY, kInImg>(a, grid, s);
       return launch_status();
     }
   }
   if constexpr (KH == 1 && KW == 1 && EPI == 0 && BN == 128 && TY == kTY) {  // convf1 from coords1's flow window
     if (a.ain == kInFlow) {
-      hipLaunchKernelGGL((conv_s32_kernel<KH, KW, BN, WM, WN, EPI, TY, kInFlow>), grid, dim3(64 * WM * WN), 0, s, a);
+      launch_staged<KH, KW, BN, WM, WN, EPI, TY, kInFlow>(a, grid, s);
       return launch_status();
     }
   }
   if constexpr (KH == 1 && KW == 1 && EPI == 0 && BN == 128) {  // convc1 on the NHWC corr lookup
     if (a.ain == kInF32) {
-      hipLaunchKernelGGL((conv_s32_kernel<KH, KW, BN, WM, WN, EPI, TY, kInF32>), grid, dim3(64 * WM * WN), 0, s, a);
+      launch_staged<KH, KW, BN, WM, WN, EPI, TY, kInF32>(a, grid, s);
       return launch_status();
     }
   }
   if (a.ain != kInS32) return OFLOW_E_MODE;
-  hipLaunchKernelGGL((conv_s32_kernel<KH, KW, BN, WM, WN, EPI, TY>), grid, dim3(64 * WM * WN), 0, s, a);
+  launch_staged<KH, KW, BN, WM, WN, EPI, TY, kInS32>(a, grid, s);
   return launch_status();
   }
 }

@@ -169,7 +169,7 @@ struct TiledArgs {
   int row;     // NHWC row pitch (floats)
 };
 
-template <int R, int OUT>
+template <int R, int OUT, bool BUF>
 __global__ __launch_bounds__(kThreads) void corr_lookup_tiled_kernel(TiledArgs a) {
   constexpr int PK = 2 * R + 2, K = 2 * R + 1, KK = K * K, PS = PK * PK;
   constexpr int QS = PS + 1;  // odd query stride
@@ -223,8 +223,12 @@ __global__ __launch_bounds__(kThreads) void corr_lookup_tiled_kernel(TiledArgs a
   __syncthreads();
 
   // ---- 2. gather ----
+  // BUF (r06, launch_tiled): every load unconditional -- a buffer load whose offset is a sentinel past this block's
+  // window reads for taps outside the level (and items past the last query) returns 0 without a memory access --
+  // instead of one exec-masked branch per load
   const float* __restrict__ Lq = base + (size_t)q0 * LF;
   float v[PER];
+  if constexpr (!BUF) {
 #pragma unroll
   for (int s = 0; s < PER; ++s) {
     const int item = tid + kThreads * s;
@@ -237,6 +241,23 @@ __global__ __launch_bounds__(kThreads) void corr_lookup_tiled_kernel(TiledArgs a
       if (q < nq && static_cast<unsigned>(y) < static_cast<unsigned>(Hl) && static_cast<unsigned>(x) < static_cast<unsigned>(Wl))
         v[s] = Lq[(size_t)q * LF + ((y >> 2) * WB + (x >> 3)) * 32 + ((y & 3) << 3) + (x & 7)];
     }
+  }
+  } else {
+  const __amdgpu_buffer_rsrc_t rsL =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(Lq), (short)0, nq * LF * 4, 0x00020000);
+#pragma unroll
+  for (int s = 0; s < PER; ++s) {
+    const int item = min(tid + kThreads * s, ITEMS - 1);  // (items past ITEMS: loaded, never stored)
+    const int q = item / PS;
+    const int rm = item - q * PS;
+    const int u = rm / PK, c = rm - u * PK;
+    const int y = sY[q] + u, x = sX[q] + c;
+    const bool in = q < nq && static_cast<unsigned>(y) < static_cast<unsigned>(Hl) &&
+                    static_cast<unsigned>(x) < static_cast<unsigned>(Wl);
+    const unsigned off = in ? static_cast<unsigned>((q * LF + ((y >> 2) * WB + (x >> 3)) * 32 + ((y & 3) << 3) + (x & 7)) * 4)
+                            : 0x80000000u;
+    v[s] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rsL, static_cast<int>(off), 0, 0));
+  }
   }
 #pragma unroll
   for (int s = 0; s < PER; ++s) {
@@ -311,13 +332,25 @@ int launch_lookup(const LookupArgs& a, hipStream_t s) {
   return launch_status();
 }
 
+// The unconditional buffer-load gathers (BUF) wherever a block's window reads fit 32-bit byte offsets (every
+// practical level: LF < 2^23 floats). r06 in-process A/B at the bench workload (tools/exp/run_lookup_buf_ab.py,
+// profiles/r06/r6s16_lookup_ab.log): cold 44.42 -> 41.79 us, hot 39.08 -> 38.15, bit-identical.
 template <int R>
 int launch_tiled(const TiledArgs& a, int out_form, hipStream_t s) {
   const dim3 grid(((a.nqb + 7) / 8) * 8 * a.nlev);
-  if (out_form == 0)
-    hipLaunchKernelGGL((corr_lookup_tiled_kernel<R, 0>), grid, dim3(kThreads), 0, s, a);
-  else
-    hipLaunchKernelGGL((corr_lookup_tiled_kernel<R, 1>), grid, dim3(kThreads), 0, s, a);
+  bool buf = true;
+  for (int l = 0; l < a.nlev; ++l) buf = buf && (long long)kQ * a.LF[l] * 4 < (1ll << 31);
+  if (buf) {
+    if (out_form == 0)
+      hipLaunchKernelGGL((corr_lookup_tiled_kernel<R, 0, true>), grid, dim3(kThreads), 0, s, a);
+    else
+      hipLaunchKernelGGL((corr_lookup_tiled_kernel<R, 1, true>), grid, dim3(kThreads), 0, s, a);
+  } else {
+    if (out_form == 0)
+      hipLaunchKernelGGL((corr_lookup_tiled_kernel<R, 0, false>), grid, dim3(kThreads), 0, s, a);
+    else
+      hipLaunchKernelGGL((corr_lookup_tiled_kernel<R, 1, false>), grid, dim3(kThreads), 0, s, a);
+  }
   return launch_status();
 }
 

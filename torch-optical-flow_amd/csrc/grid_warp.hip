@@ -400,6 +400,7 @@ __global__ __launch_bounds__(kWThreads) void warp_bilinear_lds_kernel(WarpArgs a
 // source byte is read ~1.9x from L2 (the strip's side margins and a segment's first rows) instead of ~8x with per-tile
 // bounding boxes, and with coalesced 16-B row reads. Taps outside the ring (a larger flow) are gathered from global
 // memory by that lane. Same arithmetic as grid_warp_kernel: bit-identical results.
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 constexpr int kSThreads = 1024, kSWaves = kSThreads / 64;
 constexpr int kSX = 64, kSY = 16, kSM = 28;           // strip width, rows per step, margin
 constexpr int kSRows = kSY / kSWaves;                 // output rows per thread per step
@@ -409,9 +410,23 @@ constexpr int kSC4 = kSC / 4;
 constexpr int kSMaxC = 3;
 constexpr int kSPre = (kSY * kSC4 * kSMaxC + kSThreads - 1) / kSThreads;  // float4 of a step's new rows per thread
 
+// BUF (r06, the default below 2^29 frame elements): every row and flow load unconditional -- buffer loads whose offset
+// is a sentinel past the frame's buffer for rows / chunks outside the image (the load returns zeros, no memory access)
+// -- no branch around a step's loads (past the segment's end they fetch rows nobody reads), the flow prefetched as many
+// steps ahead as the rows, and pixels whose taps leave the ring deferred to the segment's end (an LDS list), so no load
+// of a step waits for the ones issued after it. The r03 form loaded under exec-masked branches, after which the
+// compiler cannot count the outstanding loads and waits for all of them (s_waitcnt vmcnt(0), stores included) inside the
+// step loop: the rows prefetched kSD steps ahead were waited for one step later. In-process A/B at (8, 3, 436, 1024)
+// (tools/exp/run_warp_ab.py, profiles/r06/r6s16_warp_ab.log): i.i.d. N(0, 8^2) flow 33.34 -> 31.14 us, smooth 32.78 ->
+// 30.90, zero 31.70 -> 29.96; bit-identical.
+template <bool BUF>
 __global__ __launch_bounds__(kSThreads) void warp_strip_kernel(WarpArgs a, int strips, int segs, int seg_h) {
   __shared__ __attribute__((aligned(16))) float sRing[kSMaxC * kSR * kSC];
+  constexpr int kFbCap = BUF ? 1024 : 1;  // deferred out-of-ring pixels (BUF)
+  __shared__ int sFb[kFbCap];
+  __shared__ int sFbN;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  if (tid == 0) sFbN = 0;  // (published by the first step's barrier, before any append)
   // XCD-aware order: block ids equal mod 8 share an L2; each XCD takes a contiguous run of (image, strip, segment)
   const int nwg = gridDim.x, q8 = nwg / 8, r8 = nwg % 8, xcd = blockIdx.x % 8;
   int t = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + blockIdx.x / 8;
@@ -428,14 +443,23 @@ __global__ __launch_bounds__(kSThreads) void warp_strip_kernel(WarpArgs a, int s
   const float* __restrict__ fyp = a.flow + (size_t)(2 * b + 1) * HW;
 
   // one float4 of image row yy (ring slot yy mod kSR), column chunk j, channel c; rows / chunks outside the image: 0
+  // (chunks are 4-float aligned and W % 4 == 0: a chunk is wholly inside or outside a row)
+  const __amdgpu_buffer_rsrc_t rsF =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(src), (short)0, C * HW * 4, 0x00020000);
   auto fetch = [&](int c, int yy, int j) {
     const int xx = xb + 4 * j;
-    if (yy >= 0 && yy < H && xx >= 0 && xx < W)
-      return *reinterpret_cast<const float4*>(src + (size_t)c * HW + (size_t)yy * W + xx);
-    return make_float4(0.f, 0.f, 0.f, 0.f);
+    const bool in = yy >= 0 && yy < H && xx >= 0 && xx < W;
+    if constexpr (BUF) {
+      const unsigned off = in ? static_cast<unsigned>(((c * H + yy) * W + xx) * 4) : 0x80000000u;  // sentinel: zeros
+      const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rsF, static_cast<int>(off), 0, 0);
+      return make_float4(__uint_as_float(v[0]), __uint_as_float(v[1]), __uint_as_float(v[2]), __uint_as_float(v[3]));
+    } else {
+      if (in) return *reinterpret_cast<const float4*>(src + (size_t)c * HW + (size_t)yy * W + xx);
+      return make_float4(0.f, 0.f, 0.f, 0.f);
+    }
   };
   auto put = [&](int c, int yy, int j, float4 v) {
-    const int slot = ((yy % kSR) + kSR) % kSR;
+    const int slot = static_cast<int>(static_cast<unsigned>(yy + kSR) % kSR);  // (yy >= -kSM > -kSR)
     *reinterpret_cast<float4*>(&sRing[(c * kSR + slot) * kSC + 4 * j]) = v;
   };
   // rows [y, y + kSY) of every channel: item e -> (c, row, chunk)
@@ -447,10 +471,13 @@ __global__ __launch_bounds__(kSThreads) void warp_strip_kernel(WarpArgs a, int s
   auto load_rows = [&](float4 (&dst)[kSPre], int y) {
 #pragma unroll
     for (int k = 0; k < kSPre; ++k) {
-      const int e = tid + k * kSThreads;
+      const int e = BUF ? min(tid + k * kSThreads, nitems - 1) : tid + k * kSThreads;  // (BUF: past nitems unused)
       const int c = e / (kSY * kSC4), rem = e - c * (kSY * kSC4);
       const int rr = rem / kSC4, j = rem - rr * kSC4;
-      dst[k] = e < nitems ? fetch(c, y + rr, j) : make_float4(0.f, 0.f, 0.f, 0.f);
+      if constexpr (BUF)
+        dst[k] = fetch(c, y + rr, j);
+      else
+        dst[k] = e < nitems ? fetch(c, y + rr, j) : make_float4(0.f, 0.f, 0.f, 0.f);
     }
   };
   auto store_rows = [&](const float4 (&v)[kSPre], int y) {
@@ -471,10 +498,13 @@ __global__ __launch_bounds__(kSThreads) void warp_strip_kernel(WarpArgs a, int s
     float4 pv[NP];
 #pragma unroll
     for (int k = 0; k < NP; ++k) {
-      const int e = tid + k * kSThreads;
+      const int e = BUF ? min(tid + k * kSThreads, ni - 1) : tid + k * kSThreads;
       const int c = e / (R0 * kSC4), rem = e - c * (R0 * kSC4);
       const int rr = rem / kSC4, j = rem - rr * kSC4;
-      pv[k] = e < ni ? fetch(c, ys - kSM + rr, j) : make_float4(0.f, 0.f, 0.f, 0.f);
+      if constexpr (BUF)
+        pv[k] = fetch(c, ys - kSM + rr, j);
+      else
+        pv[k] = e < ni ? fetch(c, ys - kSM + rr, j) : make_float4(0.f, 0.f, 0.f, 0.f);
     }
 #pragma unroll
     for (int k = 0; k < NP; ++k) {
@@ -488,37 +518,51 @@ __global__ __launch_bounds__(kSThreads) void warp_strip_kernel(WarpArgs a, int s
 #pragma unroll
   for (int k = 1; k <= kSD; ++k) load_rows(pre[k % kSD], ys + k * kSY + kSM);
   const int xo = x0 + lane;
-  // the step's flow (wave w: rows y + w + kSWaves * h), loaded one step ahead
-  float fl[kSRows][2];
-  auto load_flow = [&](int y) {
+  // the step's flow (wave w: rows y + w + kSWaves * h), loaded FD steps ahead into FD register sets (step k: set
+  // k % FD); BUF: as far ahead as the rows (a step's flow wait then leaves the later steps' loads in flight)
+  constexpr int FD = BUF ? kSD : 1;
+  float fl[FD][kSRows][2];
+  auto load_flow = [&](float (&f)[kSRows][2], int y) {
 #pragma unroll
     for (int h = 0; h < kSRows; ++h) {
       const int yo = min(y + wave + kSWaves * h, H - 1), xc = min(xo, W - 1);
-      fl[h][0] = fxp[yo * W + xc];
-      fl[h][1] = fyp[yo * W + xc];
+      f[h][0] = fxp[yo * W + xc];
+      f[h][1] = fyp[yo * W + xc];
     }
   };
-  load_flow(ys);
+#pragma unroll
+  for (int k = 0; k < FD; ++k) load_flow(fl[k], ys + k * kSY);
 
+  // taps outside the ring: gathered from the frame (global memory)
+  auto gather_global = [&](int pix, int tx0, int ty0, unsigned m, float nw, float ne, float sw, float se) {
+    const int o = ty0 * W + tx0;
+    for (int c = 0; c < C; ++c) {
+      const float* sp = src + (size_t)c * HW + o;
+      const float v[4] = {(m & 1u) ? sp[0] : 0.f, (m & 2u) ? sp[1] : 0.f, (m & 4u) ? sp[W] : 0.f,
+                          (m & 8u) ? sp[W + 1] : 0.f};
+      dst[(size_t)c * HW + pix] = bilerp(v, nw, ne, sw, se);
+    }
+  };
   // one step at row y; Q = the register set holding step y + kSY's new rows (refilled with step y + (kSD+1)*kSY's)
   // One barrier per step: the ring holds one step of slack (kSR = the 72 rows a step reads + 16), so the rows step
   // s + 1 adds (y + kSY + kSM ..) go to the slots of rows y - kSY - kSM .., which step s - 1 read last: after this
   // step's barrier they are free, and the barrier of step s + 1 publishes them.
   auto step = [&](int y, auto Qc) -> bool {
     constexpr int Q = decltype(Qc)::value;
+    constexpr int F = ((Q + kSD - 1) % kSD) % FD;  // (step k of the segment: Q = (k + 1) % kSD)
     if (y >= ye) return false;
     __syncthreads();
-    if (y + kSY < ye) {
+    if (BUF || y + kSY < ye) {
       store_rows(pre[Q], y + kSY + kSM);
       load_rows(pre[Q], y + (kSD + 1) * kSY + kSM);
     }
     float cur[kSRows][2];
 #pragma unroll
     for (int h = 0; h < kSRows; ++h) {
-      cur[h][0] = fl[h][0];
-      cur[h][1] = fl[h][1];
+      cur[h][0] = fl[F][h][0];
+      cur[h][1] = fl[F][h][1];
     }
-    if (y + kSY < ye) load_flow(y + kSY);
+    if (BUF || y + kSY < ye) load_flow(fl[F], y + FD * kSY);
     // ---- the step's 16 rows: wave w takes rows y + w + kSWaves * h ----
 #pragma unroll
     for (int h = 0; h < kSRows; ++h) {
@@ -559,13 +603,14 @@ __global__ __launch_bounds__(kSThreads) void warp_strip_kernel(WarpArgs a, int s
           for (int c = 0; c < kSMaxC; ++c)
             if (c < C) dst[(size_t)c * HW + pix] = bilerp(v[c], nw, ne, sw, se);
         } else {
-          const int o = ty0 * W + tx0;
-          for (int c = 0; c < C; ++c) {
-            const float* sp = src + (size_t)c * HW + o;
-            const float v[4] = {(m & 1u) ? sp[0] : 0.f, (m & 2u) ? sp[1] : 0.f, (m & 4u) ? sp[W] : 0.f,
-                                (m & 8u) ? sp[W + 1] : 0.f};
-            dst[(size_t)c * HW + pix] = bilerp(v, nw, ne, sw, se);
-          }
+          // BUF: deferred to the end of the segment (an LDS list of pixels), so that no load of the step waits here
+          // for every load issued before it (vector-memory loads retire in order); a full list gathers at once
+          int slot = kFbCap;
+          if constexpr (BUF) slot = atomicAdd(&sFbN, 1);
+          if (slot < kFbCap)
+            sFb[slot] = pix;
+          else
+            gather_global(pix, tx0, ty0, m, nw, ne, sw, se);
         }
       }
     }
@@ -575,6 +620,25 @@ __global__ __launch_bounds__(kSThreads) void warp_strip_kernel(WarpArgs a, int s
     if (!step(y, std::integral_constant<int, 1>{})) break;
     if (!step(y + kSY, std::integral_constant<int, 2>{})) break;
     if (!step(y + 2 * kSY, std::integral_constant<int, 0>{})) break;
+  }
+  if constexpr (BUF) {
+    // the deferred pixels: the step's arithmetic from their flow again, taps gathered from the frame
+    __syncthreads();
+    const int n = min(sFbN, kFbCap);
+    for (int i = tid; i < n; i += kSThreads) {
+      const int pix = sFb[i], yo = pix / W, xo2 = pix - yo * W;
+      const float gx = linspace_m1_p1(xo2, W) + fxp[pix];
+      const float gy = linspace_m1_p1(yo, H) + fyp[pix];
+      const float ix = pad_coord(unnormalize(gx, W, a.ac), W, a.pad, a.ac);
+      const float iy = pad_coord(unnormalize(gy, H, a.ac), H, a.pad, a.ac);
+      const float fx = floorf(ix), fy = floorf(iy);
+      const int tx0 = to_index(fx), ty0 = to_index(fy);
+      const float wx = ix - fx, wy = iy - fy;
+      const float ex = 1.0f - wx, ey = 1.0f - wy;
+      const unsigned m = (inb(tx0, ty0, W, H) ? 1u : 0u) | (inb(tx0 + 1, ty0, W, H) ? 2u : 0u) |
+                         (inb(tx0, ty0 + 1, W, H) ? 4u : 0u) | (inb(tx0 + 1, ty0 + 1, W, H) ? 8u : 0u);
+      gather_global(pix, tx0, ty0, m, ey * ex, ey * wx, wy * ex, wy * wx);
+    }
   }
 }
 
@@ -607,8 +671,11 @@ int launch_warp(const WarpArgs& a, int mode, hipStream_t s) {
         const int seg_h = (((a.H + segs - 1) / segs) + kSY - 1) / kSY * kSY;
         segs = (a.H + seg_h - 1) / seg_h;
         if (cols * segs < (1ll << 31)) {
-          hipLaunchKernelGGL(warp_strip_kernel, dim3(static_cast<unsigned>(cols * segs)), dim3(kSThreads), 0, s, a,
-                             strips, segs, seg_h);
+          const dim3 g(static_cast<unsigned>(cols * segs));
+          if ((long long)a.C * a.H * a.W < (1ll << 29))  // (BUF: the frame's byte offsets < 2^31)
+            hipLaunchKernelGGL((warp_strip_kernel<true>), g, dim3(kSThreads), 0, s, a, strips, segs, seg_h);
+          else
+            hipLaunchKernelGGL((warp_strip_kernel<false>), g, dim3(kSThreads), 0, s, a, strips, segs, seg_h);
           break;
         }
       }
