@@ -102,6 +102,7 @@ def warp_leg(dev, reps: int = 20):
         evs = []
         for i in range(reps):
             fr, fl = pairs[i % 2]
+            torch.cuda._sleep(2_000_000)  # (as in lookup_api_leg: the events bracket the kernel, not the host's enqueue)
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record(stream)
             optical_flow.warp(fr, fl)
@@ -145,15 +146,21 @@ def lookup_api_leg(ppg: int, dims, flow_low, dev, reps: int = 12):
         blocks.append(CorrBlock(f1.to(dev), f2.to(dev)))
     coords = (coords_grid(ppg, h0, w0).to(dev) + flow_low[:ppg].float()).contiguous()
     st = torch.cuda.current_stream(dev)
-    ts = []
-    for i in range(reps + 2):
+    for i in range(2):
+        blocks[i % 2](coords)
+    torch.cuda.synchronize(dev)
+    evs = []
+    for i in range(reps):
+        # each launch queued behind a spin kernel, so that its events bracket the kernel alone and not the host's
+        # enqueue of the launch (r06: timing from an idle GPU added ~3 us of host latency to every launch)
+        torch.cuda._sleep(2_000_000)
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record(st)
         blocks[i % 2](coords)
         e1.record(st)
-        e1.synchronize()
-        if i >= 2:
-            ts.append(e0.elapsed_time(e1))
+        evs.append((e0, e1))
+    torch.cuda.synchronize(dev)
+    ts = [e0.elapsed_time(e1) for e0, e1 in evs]
     ms = statistics.fmean(ts)
     nbytes = lookup_bytes(ppg, dims)
     ach = nbytes / (ms * 1e-3) / 1e9
