@@ -232,6 +232,8 @@ __global__ __launch_bounds__(64 * WM * WN, WM * WN == 8 ? 1 : 2) void conv_s32_k
   constexpr int WHALF = WS == 2 ? (WCOLS + 1) / 2 : WCOLS, WPITCH = WS == 2 ? 2 * WHALF : WCOLS;
   constexpr int WPLANE = WROWS * WPITCH;
   constexpr int WKPAD = AIN == kInFlow ? 128 : 160;  // patch channels staged (>= 49 * WC: zeros past it)
+  constexpr int WAPER = WIN ? BM * 4 / NTH : 1;      // window input: (pixel, 8 patch channels) items per thread
+  static_assert(!WIN || (BM * 4) % NTH == 0, "window items");
   static_assert(AIN != kInImg || (WHALF == kImgHalf && WPITCH == kImgPitch && WPLANE == kImgPlane), "stem window");
   constexpr bool ADB = (T == 1) && !(WIN && OFLOW_STEM_SINGLE_A);
   // 128-B LDS rows, 16-B slots XOR-swizzled (slot ^= (row >> 1) & 7): the 32 rows of an MFMA operand read by
@@ -364,29 +366,40 @@ __global__ __launch_bounds__(64 * WM * WN, WM * WN == 8 ? 1 : 2) void conv_s32_k
   float2 af4_[4];                                                                                                    \
   if constexpr (AIN == kInF32Norm) _Pragma("unroll") for (int e_ = 0; e_ < 4; ++e_)                                  \
     af4_[e_] = sAff[(G) * 32 + 4 * (tid & 7) + e_];                                                                  \
+  if constexpr (WIN) {                                                                                               \
+    /* window input: item = (pixel p, 8 patch channels G*32 + 8cp ..), consecutive lanes on consecutive pixels       \
+       (conflict-free window reads); hi and lo each one 16-B slot of the pixel's row: with 144-B rows the 8 lanes of \
+       a ds_write_b128 phase cover the 32 banks once (4-channel items wrote 8-B halves: 2-way conflicts, twice the   \
+       writes) */                                                                                                    \
+    _Pragma("unroll") for (int s_ = 0; s_ < WAPER; ++s_) {                                                           \
+      const int item = tid + s_ * NTH;                                                                               \
+      const int p = item % BM, cp = item / BM;                                                                       \
+      const int pb_ = WS * (p >> 5) * WPITCH + (p & 31);                                                             \
+      const int4 k0_ = *reinterpret_cast<const int4*>(sKoff + (G) * 32 + 8 * cp);                                    \
+      const int4 k1_ = *reinterpret_cast<const int4*>(sKoff + (G) * 32 + 8 * cp + 4);                                \
+      const int kov_[8] = {k0_.x, k0_.y, k0_.z, k0_.w, k1_.x, k1_.y, k1_.z, k1_.w};                                  \
+      float v8_[8];                                                                                                  \
+      _Pragma("unroll") for (int e_ = 0; e_ < 8; ++e_) {                                                             \
+        v8_[e_] = sImg[kov_[e_] < 0 ? kImgZero : pb_ + kov_[e_]];                                                    \
+        amx_ = fmaxf(amx_, fabsf(v8_[e_]));                                                                          \
+      }                                                                                                              \
+      half8 h8_, l8_;                                                                                                \
+      split_vec(v8_, h8_, l8_);                                                                                      \
+      uint8_t* rw_ = sA + (BUF) * A_BYTES + p * RSA;                                                                 \
+      *reinterpret_cast<half8*>(rw_ + ((cp ^ aswz(p)) << 4)) = h8_;                                                  \
+      *reinterpret_cast<half8*>(rw_ + (((4 + cp) ^ aswz(p)) << 4)) = l8_;                                            \
+    }                                                                                                                \
+  } else                                                                                                             \
   _Pragma("unroll") for (int s_ = 0; s_ < APER; ++s_) {                                                              \
     const int item = tid + s_ * NTH;                                                                            \
-    /* image input: consecutive lanes take consecutive pixels of one chunk (conflict-free window reads); else the   \
-       8 chunks of a pixel (whole 128-B LDS rows per 8 lanes) */                                                     \
-    const int p = WIN ? item % BM : item >> 3, c = WIN ? item / BM : item & 7;                                       \
+    /* the 8 chunks of a pixel (whole 128-B LDS rows per 8 lanes) */                                                 \
+    const int p = item >> 3, c = item & 7;                                                                           \
     if (AITEMS % NTH == 0 || item < AITEMS) {                                                                   \
       if constexpr (AIN != kInS32) {                                                                                 \
         /* 4 fp32 channels (G*32 + 4c ..) [-> relu(x * scale + shift)] -> 4 hi + 4 lo halves (8 B each) */           \
         typedef _Float16 half4_ __attribute__((ext_vector_type(4)));                                                 \
         half4_ h4 = {0, 0, 0, 0}, l4 = {0, 0, 0, 0};                                                                 \
-        if constexpr (WIN) {                                                                                         \
-          /* patch channel k of pixel p = the staged window at (WS*py, WS*px) + the channel's table offset */        \
-          const int pb_ = WS * (p >> 5) * WPITCH + (p & 31);                                                         \
-          const int4 ko_ = *reinterpret_cast<const int4*>(sKoff + (G) * 32 + 4 * c);                                 \
-          const int kov_[4] = {ko_.x, ko_.y, ko_.z, ko_.w};                                                          \
-          float mx_ = 0.f, v4_[4];                                                                                   \
-          _Pragma("unroll") for (int e_ = 0; e_ < 4; ++e_) {                                                         \
-            v4_[e_] = sImg[kov_[e_] < 0 ? kImgZero : pb_ + kov_[e_]];                                                \
-            mx_ = fmaxf(mx_, fabsf(v4_[e_]));                                                                        \
-          }                                                                                                          \
-          split_vec(v4_, h4, l4);                                                                                    \
-          amx_ = fmaxf(amx_, mx_);                                                                                   \
-        } else if (((aok >> s_) & 1u) && (AIN != kInF32 || (G) * 32 + 4 * c < a.cin)) {                             \
+        if (((aok >> s_) & 1u) && (AIN != kInF32 || (G) * 32 + 4 * c < a.cin)) {                                     \
           const float* fv = reinterpret_cast<const float*>(&RA[s_]);                                                 \
           float mx_ = 0.f, v4_[4];                                                                                   \
           _Pragma("unroll") for (int e_ = 0; e_ < 4; ++e_) {                                                         \
