@@ -39,6 +39,9 @@ from .utils import coords_grid, upflow8
 # both frames, bit-identical to the reference's CPU arithmetic (ATen on the GPU divides by multiplying with fl(1/255),
 # 1 ulp off for ~74 % of values); in-process step 18.56 -> 18.48 ms (profiles/r04/s35_ab.log). False: the ATen form.
 NATIVE_NORMALIZE = True
+# the pair lanes' SplitUpdate state (cnet output packed into the GRU state, the hoisted context terms) built on the cnet
+# stream right after cnet, beside fnet's tail and the correlation pyramid, instead of on the lanes after the pyramid
+EARLY_LANE_INIT = True
 
 
 class HParams(dict):
@@ -181,34 +184,49 @@ class RAFT(nn.Module):
         up_flow = torch.sum(mask * up_flow, dim=2).permute(0, 1, 4, 2, 5, 3)
         return up_flow.reshape(n, 2, 8 * h, 8 * w)
 
-    def _split_update_lanes(self, corr_fn, cnet_out: Tensor, coords0: Tensor, coords1: Tensor, iters: int, hdim: int,
-                            test_mode: bool) -> List[Tensor]:
-        """The split update loop with the pairs in ``pair_lanes`` parts, each on its own stream (lane) with its own side stream;
-        coords1 is advanced in place. Per-pixel results are those of the single-lane loop bit for bit (no reduction
-        crosses pairs). Returns the upsampled flows (test mode: the last one only)."""
-        b = cnet_out.shape[0]
-        dev = cnet_out.device
+    def _lane_cuts(self, b: int):
         n = min(self.pair_lanes, b)
         edges = [(b * i) // n for i in range(n + 1)]
-        cuts = list(zip(edges[:-1], edges[1:]))
+        return list(zip(edges[:-1], edges[1:]))
+
+    def _lane_runners(self, cnet_out: Tensor, hdim: int, lanes, on=None) -> list:
+        """One SplitUpdate per lane (its buffers, the cnet output packed into the GRU state, the loop-invariant context
+        terms), built on stream ``on`` (default: each lane's own stream)."""
+        runners = []
+        for i, ((b0, b1), st) in enumerate(zip(self._lane_cuts(cnet_out.shape[0]), lanes)):
+            with torch.cuda.stream(on if on is not None else st):
+                slot = 0 if i == 0 else 200 + i
+                runners.append(SplitUpdate(self.update_block, cnet_out[b0:b1], hdim, side_slot=slot, fuse_c1=self.lookup_fusion,
+                                           flow_head_pixels=cnet_out.shape[0] * cnet_out.shape[2] * cnet_out.shape[3],
+                                           side_owner=st))
+        return runners
+
+    def _lanes_for(self, dev, b: int):
         main = torch.cuda.current_stream(dev)
-        lanes = [main] + [_side_stream(dev, 100 + i) for i in range(1, n)]
+        return [main] + [_side_stream(dev, 100 + i) for i in range(1, min(self.pair_lanes, b))]
+
+    def _split_update_lanes(self, corr_fn, cnet_out: Tensor, coords0: Tensor, coords1: Tensor, iters: int, hdim: int,
+                            test_mode: bool, runners=None) -> List[Tensor]:
+        """The split update loop with the pairs in ``pair_lanes`` parts, each on its own stream (lane) with its own side stream;
+        coords1 is advanced in place. Per-pixel results are those of the single-lane loop bit for bit (no reduction
+        crosses pairs). Returns the upsampled flows (test mode: the last one only). ``runners``: the lanes' SplitUpdates
+        when already built (on the cnet stream, beside the correlation pyramid; the current stream has waited for it)."""
+        b = cnet_out.shape[0]
+        dev = cnet_out.device
+        cuts = self._lane_cuts(b)
+        main = torch.cuda.current_stream(dev)
+        lanes = self._lanes_for(dev, b)
         # the packed weights (built on first use, by kernels on this stream) must exist before the lanes fork: the
         # lanes read them with no later join when the lookup is not joined (fused into convc1, or pair_lookup "lane")
         SplitUpdate._weights(self.update_block)
         # lane_init_on_main: the lanes' buffers are allocated (and their loop-invariant context terms computed) on the
         # main stream before the fork, so that no lane allocates from its own stream
-        init_main = getattr(self, "lane_init_on_main", False)
+        init_main = getattr(self, "lane_init_on_main", False) or runners is not None
         if not init_main:
             for st in lanes[1:]:
                 st.wait_stream(main)
-        runners = []
-        for i, ((b0, b1), st) in enumerate(zip(cuts, lanes)):
-            with torch.cuda.stream(main if init_main else st):
-                slot = 0 if i == 0 else 200 + i
-                runners.append(SplitUpdate(self.update_block, cnet_out[b0:b1], hdim, side_slot=slot, fuse_c1=self.lookup_fusion,
-                                           flow_head_pixels=cnet_out.shape[0] * cnet_out.shape[2] * cnet_out.shape[3],
-                                           side_owner=st))
+        if runners is None:
+            runners = self._lane_runners(cnet_out, hdim, lanes, on=main if init_main else None)
         if init_main:
             for st in lanes[1:]:
                 st.wait_stream(main)
@@ -325,6 +343,7 @@ class RAFT(nn.Module):
         fnet = SplitEncoder(self.fnet) if split_enc else self.fnet
         cnet = SplitEncoder(self.cnet) if split_enc and not self.cnet.training else self.cnet
         block = AlternateCorrBlock if self.hparams.get("alternate_corr", False) else CorrBlock
+        pre_runners = None
         if split_enc and isinstance(cnet, SplitEncoder):
             # image0's stem patches are the first rows of fnet's (raft.py:109, 115 feed both the same image0); cnet
             # runs on a side stream beside fnet and the correlation pyramid, joined before the update loop
@@ -344,10 +363,18 @@ class RAFT(nn.Module):
             else:
                 patches = None if sfi else fnet.stem_patches(torch.cat([image0, image1], dim=0))
             cpatches = None if patches is None else patches[:nb]
+            early = (EARLY_LANE_INIT and side is not None and self.fused_update and self.update_impl == "split"
+                     and self.pair_lanes > 1 and nb > 1 and block is CorrBlock and self.split_corr)
+            lanes = self._lanes_for(image0.device, nb) if early else None  # (main = the current stream, not cnet's)
             if side is not None:
                 side.wait_stream(main)
                 with torch.cuda.stream(side):
                     cnet_out = cnet(image0, patches=cpatches, stem_from_image=sfi)
+                    if early:
+                        # the lanes' GRU state and context terms depend on cnet only: built here, beside fnet's tail
+                        # and the correlation pyramid, instead of after the pyramid on the lanes
+                        SplitUpdate._weights(self.update_block)
+                        pre_runners = self._lane_runners(cnet_out, hdim, lanes, on=side)
             if block is CorrBlock and self.split_corr:
                 # features as S32 rows straight from fnet's head conv -> split-fp16 pyramid (no fp32 fmaps)
                 if side2 is not None:
@@ -377,7 +404,8 @@ class RAFT(nn.Module):
         flow_up = None
         if impl == "split" and self.pair_lanes > 1 and cnet_out.shape[0] > 1 and hasattr(corr_fn, "lookup_nhwc"):
             coords1 = coords1.contiguous()
-            flow_predictions = self._split_update_lanes(corr_fn, cnet_out, coords0, coords1, iters, hdim, test_mode)
+            flow_predictions = self._split_update_lanes(corr_fn, cnet_out, coords0, coords1, iters, hdim, test_mode,
+                                                        runners=pre_runners)
             if test_mode:
                 return coords1 - coords0, flow_predictions[-1]
             return flow_predictions
