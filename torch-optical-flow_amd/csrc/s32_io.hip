@@ -45,6 +45,7 @@ __global__ __launch_bounds__(256) void pack_s32_kernel(const float* __restrict__
   const long long p = item - c32 * P;
   const int b = static_cast<int>(p) / HW;
   const int pix = static_cast<int>(p) - b * HW;
+  const bool f16b = f != nullptr && (fcs & 3) == 0 && (reinterpret_cast<uintptr_t>(f) & 15) == 0;
 #pragma unroll
   for (int o = 0; o < 4; ++o) {
     const int c0 = c32 * 32 + o * 8;
@@ -60,9 +61,15 @@ __global__ __launch_bounds__(256) void pack_s32_kernel(const float* __restrict__
     put8(y0 + p * y0ps + off, v);
     if (y1) put8(y1 + p * y1ps + off, v);
     if (f) {
+      float* fp = f + p * fcs + c0;
+      if (f16b && c0 + 8 <= C) {  // two 16-B stores (was 8 dword stores 4 * fcs bytes apart across the lanes)
+        reinterpret_cast<float4*>(fp)[0] = make_float4(v[0], v[1], v[2], v[3]);
+        reinterpret_cast<float4*>(fp)[1] = make_float4(v[4], v[5], v[6], v[7]);
+      } else {
 #pragma unroll
-      for (int j = 0; j < 8; ++j)
-        if (c0 + j < C) f[p * fcs + c0 + j] = v[j];
+        for (int j = 0; j < 8; ++j)
+          if (c0 + j < C) fp[j] = v[j];
+      }
     }
   }
 }
