@@ -870,27 +870,49 @@ __global__ __launch_bounds__(64 * WM * WN, WM * WN == 8 ? 1 : 2) void conv_s32_k
       for (int nt = 0; nt < NT; ++nt) {
         const int nl = wn * (BN / WN) + nt * 32 + r;
         const float2 sb = sSB[nl];
-        float cnt = 0.f, sum = 0.f;
+        float cnt = 0.f, sum = 0.f, q = 0.f;
+        // a tile wholly inside the image (every tile of the 8 / 4-aligned encoder grids) skips the per-value bounds
+        // selects: the same sums in the same order (cnt = 16 * MT exactly)
+        const bool full = ty0 + TY <= a.H && tx0 + kTX <= a.W;
+        if (full) {
 #pragma unroll
-        for (int mt = 0; mt < MT; ++mt) {
-          const bool yok = ty0 + wm * MT + mt < a.H;
+          for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
-          for (int e = 0; e < 16; ++e) {
-            const bool ok = yok && tx0 + (e & 3) + 8 * (e >> 2) + 4 * hh < a.W;
-            sum += ok ? acc[mt][nt][e] * sb.x + sb.y : 0.f;
-            cnt += ok ? 1.f : 0.f;
+            for (int e = 0; e < 16; ++e) sum += acc[mt][nt][e] * sb.x + sb.y;
+          cnt = 16.f * MT;
+        } else {
+#pragma unroll
+          for (int mt = 0; mt < MT; ++mt) {
+            const bool yok = ty0 + wm * MT + mt < a.H;
+#pragma unroll
+            for (int e = 0; e < 16; ++e) {
+              const bool ok = yok && tx0 + (e & 3) + 8 * (e >> 2) + 4 * hh < a.W;
+              sum += ok ? acc[mt][nt][e] * sb.x + sb.y : 0.f;
+              cnt += ok ? 1.f : 0.f;
+            }
           }
         }
         const float mean = cnt > 0.f ? sum / cnt : 0.f;
-        float q = 0.f;
+        if (full) {
 #pragma unroll
-        for (int mt = 0; mt < MT; ++mt) {
-          const bool yok = ty0 + wm * MT + mt < a.H;
+          for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
-          for (int e = 0; e < 16; ++e) {
-            const bool ok = yok && tx0 + (e & 3) + 8 * (e >> 2) + 4 * hh < a.W;
-            const float d = (acc[mt][nt][e] * sb.x + sb.y) - mean;
-            q += ok ? d * d : 0.f;
+            for (int e = 0; e < 16; ++e) {
+              const float d = (acc[mt][nt][e] * sb.x + sb.y) - mean;
+              float dd = d * d;
+              asm volatile("" : "+v"(dd));  // no fma contraction: the checked form below rounds d * d before the add
+              q += dd;
+            }
+        } else {
+#pragma unroll
+          for (int mt = 0; mt < MT; ++mt) {
+            const bool yok = ty0 + wm * MT + mt < a.H;
+#pragma unroll
+            for (int e = 0; e < 16; ++e) {
+              const bool ok = yok && tx0 + (e & 3) + 8 * (e >> 2) + 4 * hh < a.W;
+              const float d = (acc[mt][nt][e] * sb.x + sb.y) - mean;
+              q += ok ? d * d : 0.f;
+            }
           }
         }
         // merge with lane ^ 32 (symmetric: both lanes compute the same value; lane half 0 first)
