@@ -55,6 +55,7 @@ HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 MFMA_F32_PEAK_TFLOPS = 157.3  # dense fp32 MFMA (v_mfma_f32_32x32x2_f32), spec
 MFMA_F16_PEAK_TFLOPS = 2500.0  # dense fp16 MFMA, spec (no sparsity)
 PMC_TRAFFIC_FILE = os.path.join(REPO, "profiles", "lookup_traffic.json")
+SPIN_CYCLES = 40_000_000  # torch.cuda._sleep ahead of the after-step legs: longer than the host's enqueue of their launches
 BATCH_GOLDEN = os.path.join(REPO, "tests", "golden", "raft_e2e_batch.npz")
 HD_GOLDEN = os.path.join(REPO, "tests", "golden", "raft_e2e_hd.npz")
 # the reference forward's FLOPs per pair (12 iterations, measured with the torch profiler)
@@ -82,7 +83,8 @@ def lookup_bytes(batch: int, dims, radius: int = 4, s_corr: int = 4) -> int:
 def warp_leg(dev, reps: int = 20):
     """The flow-warp operator (`optical_flow.warp`, reference operator.py:8-33) at SURVEY §8(d)'s warp workload: frame
     (8, 3, 436, 1024), flow = normalize(N(0, 8^2) px) per pixel (seeded), default modes (bilinear, border,
-    align_corners=False); timed after the timed region with HIP events on the launch stream (two frame/flow pairs
+    align_corners=False); timed after the timed region, ``reps`` launches back to back between one pair of HIP events
+    on the launch stream (two frame/flow pairs
     alternating so that no launch finds its inputs in the Infinity Cache). Algorithmic bytes (2C + 2) * 4 per pixel
     (frame read + flow read + output write)."""
     import optical_flow
@@ -99,17 +101,16 @@ def warp_leg(dev, reps: int = 20):
         for fr, fl in pairs:
             optical_flow.warp(fr, fl)
         torch.cuda.synchronize(dev)
-        evs = []
+        # (as in lookup_api_leg: the launches back to back behind a spin kernel, one event pair around them)
+        torch.cuda._sleep(SPIN_CYCLES)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
         for i in range(reps):
             fr, fl = pairs[i % 2]
-            torch.cuda._sleep(2_000_000)  # (as in lookup_api_leg: the events bracket the kernel, not the host's enqueue)
-            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            e0.record(stream)
             optical_flow.warp(fr, fl)
-            e1.record(stream)
-            evs.append((e0, e1))
+        e1.record(stream)
         torch.cuda.synchronize(dev)
-    ms = mean_ms(evs)
+    ms = e0.elapsed_time(e1) / reps
     nbytes = (2 * c + 2) * 4 * b * h * w
     ach = nbytes / (ms * 1e-3) / 1e9
     return {"note": "optical_flow.warp (HIP warp_strip kernel, bilinear/border/align_corners=False) on frame "
@@ -134,8 +135,8 @@ def lookup_api_leg(ppg: int, dims, flow_low, dev, reps: int = 12):
     """The reference's lookup operator (CorrBlock.__call__, corr.py:56-77: NCHW fp32 out) on this workload's shapes,
     timed after the timed region (in the step the lookup runs inside convc1): a (ppg, 256, H/8, W/8) feature pair
     per pyramid (synthetic features, two pyramids alternating so that no launch finds its pyramid in the 256 MiB
-    Infinity Cache), the step's own final coordinates (grid + its last low-res flow), ``reps`` launches each timed with
-    HIP events on the launch stream. Roofline = SURVEY §8(d)'s algorithmic bytes / mean launch time."""
+    Infinity Cache), the step's own final coordinates (grid + its last low-res flow), ``reps`` launches back to back
+    between one pair of HIP events on the launch stream. Roofline = SURVEY §8(d)'s algorithmic bytes / mean launch time."""
     from model import CorrBlock, synthetic
     from model.utils import coords_grid
 
@@ -149,19 +150,19 @@ def lookup_api_leg(ppg: int, dims, flow_low, dev, reps: int = 12):
     for i in range(2):
         blocks[i % 2](coords)
     torch.cuda.synchronize(dev)
-    evs = []
+    # the launches back to back, queued behind a spin kernel that keeps the GPU busy while the host enqueues them, with
+    # one event pair around them: their average is the kernel plus the dispatch boundary between launches (r06: one
+    # event pair per launch from an idle GPU added the host's enqueue latency, ~3 us; per launch behind a spin kernel
+    # the event pair itself still added ~3 us to the 30 us warp against rocprof)
+    torch.cuda._sleep(SPIN_CYCLES)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(st)
     for i in range(reps):
-        # each launch queued behind a spin kernel, so that its events bracket the kernel alone and not the host's
-        # enqueue of the launch (r06: timing from an idle GPU added ~3 us of host latency to every launch)
-        torch.cuda._sleep(2_000_000)
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        e0.record(st)
         blocks[i % 2](coords)
-        e1.record(st)
-        evs.append((e0, e1))
+    e1.record(st)
     torch.cuda.synchronize(dev)
-    ts = [e0.elapsed_time(e1) for e0, e1 in evs]
-    ms = statistics.fmean(ts)
+    ms = e0.elapsed_time(e1) / reps
+    ts = [ms] * reps
     nbytes = lookup_bytes(ppg, dims)
     ach = nbytes / (ms * 1e-3) / 1e9
     return {
